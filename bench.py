@@ -1,0 +1,219 @@
+"""bench.py -- RS encode throughput on device-resident 8 MiB tracts (BASELINE.json metric).
+
+Step = one batched RS(6,3) Encode of B=1024 stripes of 8 MiB tracts already resident in
+HBM (BASELINE configs[1]); one kernel launch per step.  N GPUs: one process per GPU, each
+encodes its own B stripes (weak scaling; stripes are independent, no collective on the
+data path -- torch.distributed is used only for the barrier and the max-over-ranks time).
+
+Prints ONE JSON line (rank 0).  `value` = data GiB/s over all ranks = N*B*k*S / t.
+`roofline` prices the encode kernel by its algorithmic HBM bytes B*(k+m)*S per launch over
+the launch time measured with HIP events on the launch stream.  `cpu_baseline` (rank 0,
+N=1 only) times the CPU restatement oracle (klauspost's AVX2 nibble-table algorithm,
+OpenMP) on a bounded sample -- a reported baseline, not the target.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from blb_amd import reedsolomon as rs  # noqa: E402
+
+GIB = float(1 << 30)
+TRACT = 8 * 1024 * 1024          # core.TractLength (internal/core/constants.go:15)
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0            # MI355X_MICROARCH.md: 6.29 TB/s measured float4 copy
+METRIC = "RS encode/decode GiB/s (device-resident 8MB tracts) at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--k", type=int, default=6)
+    p.add_argument("--m", type=int, default=3)
+    p.add_argument("--batch", type=int, default=1024, help="stripes per GPU")
+    p.add_argument("--shard", type=int, default=TRACT)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-extra", action="store_true", help="skip decode / PCIe side measurements")
+    return p.parse_args()
+
+
+def pmc_traffic(k, m, batch, shard):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary, if one exists for this
+    exact workload (profiles/pmc_*.json, written by tools/pmc_summary.py)."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for fn in sorted(os.listdir(pdir), reverse=True):
+        if fn.startswith("pmc_") and fn.endswith(".json"):
+            try:
+                d = json.load(open(os.path.join(pdir, fn)))
+            except (OSError, ValueError):
+                continue
+            w = d.get("workload", {})
+            if (w.get("k"), w.get("m"), w.get("batch"), w.get("shard")) == (k, m, batch, shard):
+                return d.get("hbm_bytes_per_launch")
+    return None
+
+
+def cpu_baseline(k, m, seconds):
+    """klauspost's algorithm (AVX2 vpshufb nibble tables, OpenMP byte-range split like
+    codeSomeShardsP) from the oracle restatement, on a bounded sample of the workload."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    nstripes = 4
+    rng = np.random.default_rng(97531)
+    rows = O.build_matrix(k, m)[k:]
+    stripes = []
+    for _ in range(nstripes):
+        data = [rng.integers(0, 256, TRACT, dtype=np.uint8) for _ in range(k)]
+        par = [np.empty(TRACT, np.uint8) for _ in range(m)]
+        stripes.append((data, par))
+    O.code(rows, stripes[0][0], stripes[0][1], use_avx2=True, threads=threads)  # warm
+    done, t0 = 0, time.perf_counter()
+    while True:
+        for data, par in stripes:
+            O.code(rows, data, par, use_avx2=True, threads=threads)
+        done += nstripes
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gibps = done * k * TRACT / GIB / el
+    return {"value": round(gibps, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "avx2": bool(O.lib().rso_have_avx2()),
+            "sample": f"RS({k},{m}) encode of {done} stripes x {k}x8MiB "
+                      f"({done * k * TRACT / GIB:.1f} GiB data, {el:.1f} s) by the oracle's "
+                      f"klauspost-AVX2 restatement, {threads} OpenMP threads"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    k, m, B, S = a.k, a.m, a.batch, a.shard
+    enc = rs.New(k, m)
+    stripes = torch.empty((B, k + m, S), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(97531 * (rank + 1))
+    stripes[:, :k].random_(0, 256, generator=g)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(a.warmup):
+        enc.EncodeBatch(stripes)
+    torch.cuda.synchronize(dev)
+    ok = bool(enc.VerifyBatch(stripes).all())
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for s, e in evs:
+        s.record(stream)
+        enc.EncodeBatch(stripes)
+        e.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    launch_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    algo_bytes = B * (k + m) * S
+    achieved_gbs = algo_bytes / (launch_ms * 1e-3) / 1e9
+    data_bytes_total = world * B * k * S * a.steps
+    value = data_bytes_total / GIB / dt
+
+    extra = {}
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_extra:
+        # BASELINE config 3: ReconstructData of data shard 1 over the same batch.
+        present = [i != 1 for i in range(k + m)]
+        enc.ReconstructBatch(stripes, present, data_only=True)
+        torch.cuda.synchronize(dev)
+        dev_evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(max(3, a.steps // 2))]
+        for s, e in dev_evs:
+            s.record(stream)
+            enc.ReconstructBatch(stripes, present, data_only=True)
+            e.record(stream)
+        torch.cuda.synchronize(dev)
+        dec_ms = float(np.mean([s.elapsed_time(e) for s, e in dev_evs]))
+        extra["reconstruct_1_data_erasure"] = {
+            "GiBps_data": round(B * k * S / GIB / (dec_ms * 1e-3), 2),
+            "ms_per_launch": round(dec_ms, 3),
+            "hbm_GBps_algorithmic": round(B * (k + 1) * S / (dec_ms * 1e-3) / 1e9, 1)}
+        # BASELINE config 5 shape on one GPU: PCIe-inclusive streaming from pinned host.
+        nb = 16
+        pinned = torch.empty((nb, k + m, S), dtype=torch.uint8).pin_memory()
+        pinned[:, :k].copy_(stripes[:nb, :k].cpu())
+        host = pinned.numpy()
+        lists = [[host[b, i] for i in range(k + m)] for b in range(nb)]
+        enc.EncodeHostBatch(lists, nstreams=3)
+        t1 = time.perf_counter()
+        enc.EncodeHostBatch(lists, nstreams=3)
+        el = time.perf_counter() - t1
+        extra["pcie_inclusive_encode"] = {
+            "GiBps_data": round(nb * k * S / GIB / el, 2), "stripes": nb,
+            "note": "pinned host -> H2D -> kernel -> D2H, 3 streams; not the bench value"}
+        del pinned
+        cpu = cpu_baseline(k, m, a.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded uniform random bytes, device-resident)",
+            "config": {"workload": f"RS({k},{m}) encode, batch={B} stripes of {S // (1 << 20)} MiB tracts per GPU",
+                       "k": k, "m": m, "batch_per_gpu": B, "shard_bytes": S,
+                       "parallelism": f"stripe-batch split x{world} (no collective)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                         "frac_vs_measured_copy": round(achieved_gbs / HBM_COPY_GBS, 4),
+                         "kernel_ms": round(launch_ms, 3),
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "traffic": pmc_traffic(k, m, B, S)},
+            "cpu_baseline": cpu,
+            "verify_ok": ok,
+        }
+        if extra:
+            line["extra"] = extra
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,58 @@
+"""ctypes binding of libblbrs.so (include/blb_rs.h).
+
+There is no CPU fallback: if the HIP library is missing, importing the engine fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libblbrs.so")
+
+# Every symbol include/blb_rs.h declares, with its ctypes signature.
+_P = ctypes.c_void_p
+_SZ = ctypes.c_size_t
+_I = ctypes.c_int
+SIGNATURES = {
+    "blbrs_new": (_I, [_I, _I, ctypes.POINTER(_P)]),
+    "blbrs_free": (None, [_P]),
+    "blbrs_data_shards": (_I, [_P]),
+    "blbrs_parity_shards": (_I, [_P]),
+    "blbrs_matrix": (_I, [_P, _P, _SZ]),
+    "blbrs_encode": (_I, [_P, _P, _P]),
+    "blbrs_verify": (_I, [_P, _P, _P, ctypes.POINTER(_I)]),
+    "blbrs_reconstruct": (_I, [_P, _P, _P]),
+    "blbrs_reconstruct_data": (_I, [_P, _P, _P]),
+    "blbrs_encode_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P]),
+    "blbrs_encode_dev_ptrs": (_I, [_P, _P, _SZ, _SZ, _P]),
+    "blbrs_reconstruct_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P, _I, _P]),
+    "blbrs_reconstruct_dev_ptrs": (_I, [_P, _P, _SZ, _SZ, _P, _I, _P]),
+    "blbrs_verify_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P, _P]),
+    "blbrs_verify_dev_ptrs": (_I, [_P, _P, _SZ, _SZ, _P, _P]),
+    "blbrs_encode_host_batch": (_I, [_P, _P, _SZ, _SZ, _I]),
+    "blbrs_set_device": (_I, [_I]),
+    "blbrs_device_count": (_I, [ctypes.POINTER(_I)]),
+    "blbrs_last_error": (ctypes.c_char_p, []),
+    "blbrs_version": (ctypes.c_char_p, []),
+    "blbrs_strerror": (ctypes.c_char_p, [_I]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libblbrs.so (built by `make -C blb_amd` / __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"blb_amd: HIP engine library not built ({LIB_PATH} missing); run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C blb_amd`")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib

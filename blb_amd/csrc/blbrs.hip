@@ -1,0 +1,822 @@
+// blbrs.hip -- host runtime + C ABI (include/blb_rs.h) of the MI355X RS engine.
+//
+// What lives here (the kernels are in rs_kernels.hip):
+//   * reedsolomon.New equivalent: (k+m) x k matrix build (gf256.hpp), argument checks with
+//     klauspost's error values.
+//   * Coding plans: for each (operation, erasure pattern) the coefficient rows, their
+//     v_perm lookup tables and shard index lists, uploaded once per device and cached on
+//     the encoder -- the counterpart of klauspost's inversion tree (decode matrices
+//     cached by invalid-index set) but holding device-ready tables.
+//   * Host-memory Encoder methods (Encode / Verify / Reconstruct / ReconstructData) with
+//     klauspost's shard conventions, each call borrowing a per-device stream worker so
+//     concurrent callers (goroutines through cgo) never share a stream.
+//   * Device-resident batched entry points on caller streams, and the pinned-host
+//     streaming encoder (H2D / kernel / D2H overlapped over several streams).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/blb_rs.h"
+#include "gf256.hpp"
+#include "rs_kernels.hpp"
+
+using namespace blbrs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    g_last_error = m;
+    return BLBRS_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                         \
+    do {                                                      \
+        hipError_t e_ = (expr);                               \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr);     \
+    } while (0)
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------------------------------
+// Coding plans
+// ---------------------------------------------------------------------------------------
+
+// One kernel pass: <= kMaxRows output rows over k_in inputs.
+struct Pass {
+    int k_in = 0, rows = 0;
+    std::vector<int32_t> in_idx, out_idx;
+    std::vector<uint32_t> tables;
+};
+
+// Host description of an operation: rows x k_in coefficients, split into passes.
+struct HostPlan {
+    int k_in = 0;
+    std::vector<int32_t> in_idx;   // inputs (shard indices)
+    std::vector<int32_t> out_idx;  // outputs (shard indices), one per row
+    Mat rows;                      // out_idx.size() x k_in
+    std::vector<Pass> passes;
+};
+
+void split_passes(HostPlan& p) {
+    const int nrows = static_cast<int>(p.out_idx.size());
+    for (int r0 = 0; r0 < nrows; r0 += kMaxRows) {
+        Pass ps;
+        ps.k_in = p.k_in;
+        ps.rows = std::min(kMaxRows, nrows - r0);
+        ps.in_idx = p.in_idx;
+        ps.out_idx.assign(p.out_idx.begin() + r0, p.out_idx.begin() + r0 + ps.rows);
+        Mat sub(p.rows.begin() + static_cast<size_t>(r0) * p.k_in,
+                p.rows.begin() + static_cast<size_t>(r0 + ps.rows) * p.k_in);
+        ps.tables = perm_tables(sub, ps.rows, p.k_in);
+        p.passes.push_back(std::move(ps));
+    }
+}
+
+// Device copy of a HostPlan on one device.
+struct DevPass {
+    void* mem = nullptr;
+    const int32_t* in_idx = nullptr;
+    const int32_t* out_idx = nullptr;
+    const uint32_t* tables = nullptr;
+    int k_in = 0, rows = 0;
+};
+struct DevPlan {
+    std::vector<DevPass> passes;
+    int device = -1;
+    ~DevPlan() {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return;
+        if (hipSetDevice(device) != hipSuccess) return;
+        for (auto& p : passes)
+            if (p.mem) (void)hipFree(p.mem);
+        (void)hipSetDevice(cur);
+    }
+};
+
+int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
+    auto dp = std::make_unique<DevPlan>();
+    dp->device = device;
+    for (const Pass& ps : hp.passes) {
+        DevPass d;
+        d.k_in = ps.k_in;
+        d.rows = ps.rows;
+        const size_t n_in = ps.in_idx.size() * 4, n_out = round_up(ps.out_idx.size() * 4, 16);
+        const size_t off_out = round_up(n_in, 16), off_tab = off_out + n_out;
+        const size_t bytes = off_tab + ps.tables.size() * 4;
+        std::vector<uint8_t> host(bytes, 0);
+        std::memcpy(host.data(), ps.in_idx.data(), n_in);
+        std::memcpy(host.data() + off_out, ps.out_idx.data(), ps.out_idx.size() * 4);
+        std::memcpy(host.data() + off_tab, ps.tables.data(), ps.tables.size() * 4);
+        HIP_TRY(hipMalloc(&d.mem, bytes));
+        dp->passes.push_back(d);  // owned from here on (freed by ~DevPlan)
+        HIP_TRY(hipMemcpy(d.mem, host.data(), bytes, hipMemcpyHostToDevice));
+        auto* base = static_cast<uint8_t*>(d.mem);
+        dp->passes.back().in_idx = reinterpret_cast<const int32_t*>(base);
+        dp->passes.back().out_idx = reinterpret_cast<const int32_t*>(base + off_out);
+        dp->passes.back().tables = reinterpret_cast<const uint32_t*>(base + off_tab);
+    }
+    out = std::move(dp);
+    return BLBRS_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Encoder
+// ---------------------------------------------------------------------------------------
+
+struct blbrs_encoder {
+    int k = 0, m = 0;
+    Mat matrix;  // (k+m) x k systematic encoding matrix
+    std::mutex mu;
+    std::map<std::string, std::shared_ptr<HostPlan>> host_plans;
+    std::map<std::pair<int, std::string>, std::unique_ptr<DevPlan>> dev_plans;
+
+    // Encode / Verify: parity rows of M over the k data shards.
+    std::shared_ptr<HostPlan> encode_plan() {
+        std::lock_guard<std::mutex> g(mu);
+        auto& slot = host_plans["E"];
+        if (!slot) {
+            auto p = std::make_shared<HostPlan>();
+            p->k_in = k;
+            for (int i = 0; i < k; ++i) p->in_idx.push_back(i);
+            for (int i = 0; i < m; ++i) p->out_idx.push_back(k + i);
+            p->rows.assign(matrix.begin() + static_cast<size_t>(k) * k, matrix.end());
+            split_passes(*p);
+            slot = p;
+        }
+        return slot;
+    }
+
+    // Reconstruct(dataOnly): inputs = first k present shards ascending (klauspost
+    // reedsolomon.go reconstruct), rows = inv(M[valid]) rows of missing data shards, then
+    // (unless data_only) P[j] * inv(M[valid]) for missing parity j -- one pass produces
+    // every missing shard straight from the k survivors.  Returns nullptr + rc on error.
+    std::shared_ptr<HostPlan> decode_plan(const std::vector<uint8_t>& present, bool data_only, int* rc) {
+        std::string key(present.size() + 2, '0');
+        key[0] = 'R';
+        key[1] = data_only ? 'd' : 'a';
+        for (size_t i = 0; i < present.size(); ++i) key[i + 2] = present[i] ? '1' : '0';
+        std::lock_guard<std::mutex> g(mu);
+        auto& slot = host_plans[key];
+        if (slot) return slot;
+        auto p = std::make_shared<HostPlan>();
+        const int n = k + m;
+        for (int i = 0; i < n && static_cast<int>(p->in_idx.size()) < k; ++i)
+            if (present[i]) p->in_idx.push_back(i);
+        Mat sub(static_cast<size_t>(k) * k), dec;
+        for (int r = 0; r < k; ++r)
+            std::memcpy(&sub[static_cast<size_t>(r) * k], &matrix[static_cast<size_t>(p->in_idx[r]) * k], k);
+        if (!invert(sub, k, dec)) {
+            host_plans.erase(key);
+            *rc = fail(BLBRS_ERR_SINGULAR, "matrix is singular");
+            return nullptr;
+        }
+        p->k_in = k;
+        for (int i = 0; i < k; ++i)
+            if (!present[i]) {
+                p->out_idx.push_back(i);
+                p->rows.insert(p->rows.end(), dec.begin() + static_cast<size_t>(i) * k,
+                               dec.begin() + static_cast<size_t>(i + 1) * k);
+            }
+        if (!data_only)
+            for (int i = k; i < n; ++i)
+                if (!present[i]) {
+                    Mat prow(matrix.begin() + static_cast<size_t>(i) * k,
+                             matrix.begin() + static_cast<size_t>(i + 1) * k);
+                    Mat r = matmul(prow, 1, k, dec, k);
+                    p->out_idx.push_back(i);
+                    p->rows.insert(p->rows.end(), r.begin(), r.end());
+                }
+        split_passes(*p);
+        slot = p;
+        return slot;
+    }
+
+    // Device tables for `hp` on `device` (uploaded on first use).
+    int dev_plan(const std::string& key, const HostPlan& hp, int device, const DevPlan** out) {
+        std::lock_guard<std::mutex> g(mu);
+        auto& slot = dev_plans[{device, key}];
+        if (!slot) {
+            int rc = upload(hp, device, slot);
+            if (rc != BLBRS_OK) {
+                dev_plans.erase({device, key});
+                return rc;
+            }
+        }
+        *out = slot.get();
+        return BLBRS_OK;
+    }
+};
+
+namespace {
+
+std::string plan_key(bool encode, const std::vector<uint8_t>& present, bool data_only) {
+    if (encode) return "E";
+    std::string key(present.size() + 2, '0');
+    key[0] = 'R';
+    key[1] = data_only ? 'd' : 'a';
+    for (size_t i = 0; i < present.size(); ++i) key[i + 2] = present[i] ? '1' : '0';
+    return key;
+}
+
+// Addressing of one batch of stripes on the device.
+struct Stripes {
+    uint8_t* base = nullptr;  // strided form
+    uint64_t shard_stride = 0, stripe_stride = 0;
+    const uint64_t* ptrs = nullptr;  // device pointer table form
+    uint32_t nshards = 0;
+    bool aligned = false;
+};
+
+// Launch every pass of `plan` over `batch` stripes (split so B * tiles fits 32 bits).
+int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mode mode,
+             int32_t* mismatch, hipStream_t stream) {
+    if (batch == 0 || S == 0) return BLBRS_OK;
+    const uint64_t tps = (S + tile_bytes() - 1) / tile_bytes();
+    const uint64_t max_b = std::max<uint64_t>(1, 0xFFFFFFFFull / tps);
+    for (size_t b0 = 0; b0 < batch; b0 += max_b) {
+        const size_t nb = std::min<uint64_t>(max_b, batch - b0);
+        for (const DevPass& ps : plan.passes) {
+            CodeArgs a{};
+            a.tables = ps.tables;
+            a.in_idx = ps.in_idx;
+            a.out_idx = ps.out_idx;
+            if (st.base) {
+                a.base = st.base + b0 * st.stripe_stride;
+            } else {
+                a.ptrs = st.ptrs + b0 * st.nshards;
+            }
+            a.shard_stride = st.shard_stride;
+            a.stripe_stride = st.stripe_stride;
+            a.nshards = st.nshards;
+            a.B = static_cast<uint32_t>(nb);
+            a.S = S;
+            a.tiles_per_stripe = static_cast<uint32_t>(tps);
+            a.k = ps.k_in;
+            a.rows = ps.rows;
+            a.aligned = st.aligned ? 1 : 0;
+            a.mismatch = mismatch ? mismatch + b0 : nullptr;
+            hipError_t e = launch_code(a, mode, stream);
+            if (e != hipSuccess) return hip_fail(e, "launch rs_code_kernel");
+        }
+    }
+    return BLBRS_OK;
+}
+
+// ---- per-device resources ----
+
+// Stream worker for host-memory calls: its own streams and device staging buffer.
+struct Worker {
+    hipStream_t s[2] = {nullptr, nullptr};
+    uint8_t* dbuf = nullptr;
+    size_t cap = 0;
+    int32_t* dflag = nullptr;
+    int device = -1;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return BLBRS_OK;
+        if (dbuf) (void)hipFree(dbuf);
+        dbuf = nullptr;
+        cap = 0;
+        HIP_TRY(hipMalloc(&dbuf, bytes));
+        cap = bytes;
+        return BLBRS_OK;
+    }
+};
+
+// Pinned + device slot for uploading pointer tables of the *_ptrs entry points.
+struct PtrSlot {
+    std::mutex mu;
+    uint64_t* host = nullptr;
+    uint64_t* dev = nullptr;
+    size_t cap = 0;  // entries
+    hipEvent_t done = nullptr;
+};
+
+struct Device {
+    std::mutex mu;
+    std::vector<Worker*> idle;
+    static constexpr int kSlots = 8;
+    PtrSlot slots[kSlots];
+    std::atomic<unsigned> next_slot{0};
+};
+
+std::mutex g_dev_mu;
+std::map<int, Device*> g_devices;  // never freed (process lifetime)
+
+Device& device_ctx(int dev) {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    auto& d = g_devices[dev];
+    if (!d) d = new Device();
+    return *d;
+}
+
+int current_device(int* dev) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) return fail(BLBRS_ERR_NO_DEVICE, "no HIP device visible");
+    HIP_TRY(hipGetDevice(dev));
+    return BLBRS_OK;
+}
+
+struct WorkerLease {
+    Device* d = nullptr;
+    Worker* w = nullptr;
+    ~WorkerLease() {
+        if (w) {
+            std::lock_guard<std::mutex> g(d->mu);
+            d->idle.push_back(w);
+        }
+    }
+};
+
+int lease_worker(WorkerLease& lease) {
+    int dev = 0;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    Device& d = device_ctx(dev);
+    lease.d = &d;
+    {
+        std::lock_guard<std::mutex> g(d.mu);
+        if (!d.idle.empty()) {
+            lease.w = d.idle.back();
+            d.idle.pop_back();
+            return BLBRS_OK;
+        }
+    }
+    auto* w = new Worker();
+    w->device = dev;
+    for (auto& s : w->s) HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_TRY(hipMalloc(&w->dflag, sizeof(int32_t)));
+    lease.w = w;
+    return BLBRS_OK;
+}
+
+// klauspost checkShards / shardSize.
+int check_shards(int n, const size_t* lens, bool nilok, size_t* size) {
+    size_t s = 0;
+    for (int i = 0; i < n; ++i)
+        if (lens[i]) { s = lens[i]; break; }
+    if (s == 0) return fail(BLBRS_ERR_SHARD_NO_DATA, "no shard data");
+    for (int i = 0; i < n; ++i)
+        if (lens[i] != s && (lens[i] != 0 || !nilok)) return fail(BLBRS_ERR_SHARD_SIZE, "shard sizes do not match");
+    *size = s;
+    return BLBRS_OK;
+}
+
+bool aligned16(uintptr_t x) { return (x & 15u) == 0; }
+
+// Host-memory coding: copy the plan's inputs in, run it, copy its outputs back (or verify).
+// The shard is processed in column chunks alternating over two streams so the H2D of
+// chunk j+1 overlaps the kernel and D2H of chunk j.
+int host_code(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, uint8_t* const* shards,
+              size_t S, Mode mode, int* ok) {
+    WorkerLease lease;
+    int rc = lease_worker(lease);
+    if (rc) return rc;
+    Worker& w = *lease.w;
+    const DevPlan* plan = nullptr;
+    if ((rc = enc->dev_plan(key, hp, w.device, &plan))) return rc;
+
+    const int n = enc->k + enc->m;
+    const size_t Sp = round_up(S, 256);  // padded shard stride keeps every shard 16B-aligned
+    if ((rc = w.ensure(static_cast<size_t>(n) * Sp))) return rc;
+    const size_t chunk = S <= (size_t{2} << 20) ? S : (size_t{1} << 20);
+    std::vector<bool> is_out(n, false);
+    for (int32_t o : hp.out_idx) is_out[o] = true;
+
+    if (mode == Mode::kVerify) HIP_TRY(hipMemsetAsync(w.dflag, 0, sizeof(int32_t), w.s[0]));
+    hipEvent_t ev = nullptr;
+    if (mode == Mode::kVerify) {
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ev, w.s[0]));
+        HIP_TRY(hipStreamWaitEvent(w.s[1], ev, 0));
+    }
+    int j = 0;
+    for (size_t off = 0; off < S; off += chunk, ++j) {
+        const size_t len = std::min(chunk, S - off);
+        hipStream_t s = w.s[j & 1];
+        for (int32_t i : hp.in_idx)
+            HIP_TRY(hipMemcpyAsync(w.dbuf + static_cast<size_t>(i) * Sp + off, shards[i] + off, len,
+                                   hipMemcpyHostToDevice, s));
+        if (mode == Mode::kVerify)
+            for (int32_t i : hp.out_idx)
+                HIP_TRY(hipMemcpyAsync(w.dbuf + static_cast<size_t>(i) * Sp + off, shards[i] + off, len,
+                                       hipMemcpyHostToDevice, s));
+        Stripes st;
+        st.base = w.dbuf + off;
+        st.shard_stride = Sp;
+        st.stripe_stride = static_cast<uint64_t>(n) * Sp;
+        st.aligned = aligned16(off);
+        if ((rc = run_plan(*plan, st, 1, len, mode, w.dflag, s))) return rc;
+        if (mode == Mode::kStore)
+            for (int32_t i : hp.out_idx)
+                HIP_TRY(hipMemcpyAsync(shards[i] + off, w.dbuf + static_cast<size_t>(i) * Sp + off, len,
+                                       hipMemcpyDeviceToHost, s));
+    }
+    int32_t flag = 0;
+    if (mode == Mode::kVerify) {
+        HIP_TRY(hipEventRecord(ev, w.s[1]));
+        HIP_TRY(hipStreamWaitEvent(w.s[0], ev, 0));
+        HIP_TRY(hipMemcpyAsync(&flag, w.dflag, sizeof(int32_t), hipMemcpyDeviceToHost, w.s[0]));
+    }
+    HIP_TRY(hipStreamSynchronize(w.s[0]));
+    HIP_TRY(hipStreamSynchronize(w.s[1]));
+    if (ev) (void)hipEventDestroy(ev);
+    if (ok) *ok = flag ? 0 : 1;
+    return BLBRS_OK;
+}
+
+// Upload a host array of device pointers to a device pointer table on `stream`.  The
+// slot's event keeps it busy until the kernels that read it have run.
+struct PtrLease {
+    PtrSlot* slot = nullptr;
+    hipStream_t stream = nullptr;
+    ~PtrLease() {
+        if (slot) {
+            (void)hipEventRecord(slot->done, stream);
+            slot->mu.unlock();
+        }
+    }
+};
+
+int upload_ptrs(uint8_t* const* ptrs, size_t count, hipStream_t stream, PtrLease& lease,
+                const uint64_t** dev_out, bool* aligned) {
+    int dev = 0;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    Device& d = device_ctx(dev);
+    PtrSlot& s = d.slots[d.next_slot.fetch_add(1) % Device::kSlots];
+    s.mu.lock();
+    if (!s.done) {
+        hipError_t e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        if (e != hipSuccess) { s.mu.unlock(); return hip_fail(e, "hipEventCreate"); }
+    } else {
+        hipError_t e = hipEventSynchronize(s.done);
+        if (e != hipSuccess) { s.mu.unlock(); return hip_fail(e, "hipEventSynchronize"); }
+    }
+    if (s.cap < count) {
+        if (s.host) (void)hipHostFree(s.host);
+        if (s.dev) (void)hipFree(s.dev);
+        s.host = nullptr;
+        s.dev = nullptr;
+        s.cap = 0;
+        const size_t cap = std::max<size_t>(count, 1024);
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&s.host), cap * 8, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.dev), cap * 8);
+        if (e != hipSuccess) { s.mu.unlock(); return hip_fail(e, "ptr table alloc"); }
+        s.cap = cap;
+    }
+    bool al = true;
+    for (size_t i = 0; i < count; ++i) {
+        if (!ptrs[i]) { s.mu.unlock(); return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer"); }
+        s.host[i] = reinterpret_cast<uint64_t>(ptrs[i]);
+        al = al && aligned16(s.host[i]);
+    }
+    lease.slot = &s;
+    lease.stream = stream;
+    HIP_TRY(hipMemcpyAsync(s.dev, s.host, count * 8, hipMemcpyHostToDevice, stream));
+    *dev_out = s.dev;
+    *aligned = al;
+    return BLBRS_OK;
+}
+
+int current_dev_or_fail(int* dev) { return current_device(dev); }
+
+std::vector<uint8_t> present_vec(const blbrs_encoder* enc, const uint8_t* present) {
+    std::vector<uint8_t> p(enc->k + enc->m);
+    for (int i = 0; i < enc->k + enc->m; ++i) p[i] = present[i] ? 1 : 0;
+    return p;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------
+extern "C" {
+
+int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out) {
+    if (!out) return fail(BLBRS_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    if (data_shards <= 0 || parity_shards <= 0)
+        return fail(BLBRS_ERR_INV_SHARD_NUM, "cannot create Encoder with zero or less data/parity shards");
+    if (data_shards + parity_shards > 256)
+        return fail(BLBRS_ERR_MAX_SHARD_NUM, "cannot create Encoder with more than 256 data+parity shards");
+    auto* e = new blbrs_encoder();
+    e->k = data_shards;
+    e->m = parity_shards;
+    if (!build_matrix(data_shards, parity_shards, e->matrix)) {
+        delete e;
+        return fail(BLBRS_ERR_SINGULAR, "matrix is singular");
+    }
+    *out = e;
+    return BLBRS_OK;
+}
+
+void blbrs_free(blbrs_encoder* enc) { delete enc; }
+int blbrs_data_shards(const blbrs_encoder* enc) { return enc ? enc->k : 0; }
+int blbrs_parity_shards(const blbrs_encoder* enc) { return enc ? enc->m : 0; }
+
+int blbrs_matrix(const blbrs_encoder* enc, uint8_t* out, size_t cap) {
+    if (!enc || !out) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (cap < enc->matrix.size()) return fail(BLBRS_ERR_INVALID_ARG, "buffer too small");
+    std::memcpy(out, enc->matrix.data(), enc->matrix.size());
+    return BLBRS_OK;
+}
+
+int blbrs_encode(blbrs_encoder* enc, uint8_t* const* shards, const size_t* lens) {
+    if (!enc || !shards || !lens) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    const int n = enc->k + enc->m;
+    size_t S = 0;
+    int rc = check_shards(n, lens, false, &S);
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i)
+        if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
+    auto hp = enc->encode_plan();
+    return host_code(enc, "E", *hp, shards, S, Mode::kStore, nullptr);
+}
+
+int blbrs_verify(blbrs_encoder* enc, const uint8_t* const* shards, const size_t* lens, int* ok) {
+    if (!enc || !shards || !lens || !ok) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    const int n = enc->k + enc->m;
+    size_t S = 0;
+    int rc = check_shards(n, lens, false, &S);
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i)
+        if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
+    auto hp = enc->encode_plan();
+    return host_code(enc, "E", *hp, const_cast<uint8_t* const*>(shards), S, Mode::kVerify, ok);
+}
+
+static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens, bool data_only) {
+    if (!enc || !shards || !lens) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    const int n = enc->k + enc->m;
+    size_t S = 0;
+    int rc = check_shards(n, lens, true, &S);
+    if (rc) return rc;
+    std::vector<uint8_t> present(n);
+    int npresent = 0;
+    for (int i = 0; i < n; ++i) {
+        present[i] = lens[i] != 0;
+        npresent += present[i];
+    }
+    if (npresent == n) return BLBRS_OK;
+    if (npresent < enc->k) return fail(BLBRS_ERR_TOO_FEW_SHARDS, "too few shards given");
+    auto hp = enc->decode_plan(present, data_only, &rc);
+    if (!hp) return rc;
+    for (int32_t i : hp->in_idx)
+        if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
+    for (int32_t i : hp->out_idx)
+        if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "missing shard has no output buffer");
+    if (hp->out_idx.empty()) return BLBRS_OK;  // data_only with only parity missing
+    rc = host_code(enc, plan_key(false, present, data_only), *hp, shards, S, Mode::kStore, nullptr);
+    if (rc) return rc;
+    for (int32_t i : hp->out_idx) lens[i] = S;
+    return BLBRS_OK;
+}
+
+int blbrs_reconstruct(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens) {
+    return reconstruct_host(enc, shards, lens, false);
+}
+
+int blbrs_reconstruct_data(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens) {
+    return reconstruct_host(enc, shards, lens, true);
+}
+
+// ---- device-resident batched path ----
+
+static int dev_stripes_strided(const blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
+                               size_t stripe_stride, size_t batch, size_t shard_len, Stripes* st) {
+    if (!stripes) return fail(BLBRS_ERR_INVALID_ARG, "stripes is NULL");
+    const int n = enc->k + enc->m;
+    if (shard_stride < shard_len || (batch > 1 && stripe_stride < shard_len))
+        return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than shard length");
+    (void)n;
+    st->base = stripes;
+    st->shard_stride = shard_stride;
+    st->stripe_stride = stripe_stride;
+    st->aligned = aligned16(reinterpret_cast<uintptr_t>(stripes)) && aligned16(shard_stride) &&
+                  aligned16(stripe_stride);
+    return BLBRS_OK;
+}
+
+static int dev_run(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, const Stripes& st,
+                   size_t batch, size_t S, Mode mode, int32_t* mismatch, void* stream) {
+    int dev = 0;
+    int rc = current_dev_or_fail(&dev);
+    if (rc) return rc;
+    const DevPlan* plan = nullptr;
+    if ((rc = enc->dev_plan(key, hp, dev, &plan))) return rc;
+    return run_plan(*plan, st, batch, S, mode, mismatch, static_cast<hipStream_t>(stream));
+}
+
+int blbrs_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                     size_t batch, size_t shard_len, void* stream) {
+    if (!enc) return fail(BLBRS_ERR_INVALID_ARG, "enc is NULL");
+    if (batch == 0 || shard_len == 0) return BLBRS_OK;
+    Stripes st;
+    int rc = dev_stripes_strided(enc, stripes, shard_stride, stripe_stride, batch, shard_len, &st);
+    if (rc) return rc;
+    auto hp = enc->encode_plan();
+    return dev_run(enc, "E", *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+}
+
+int blbrs_encode_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
+                          void* stream) {
+    if (!enc || !shard_ptrs) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (batch == 0 || shard_len == 0) return BLBRS_OK;
+    const int n = enc->k + enc->m;
+    PtrLease lease;
+    Stripes st;
+    int rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, &st.ptrs, &st.aligned);
+    if (rc) return rc;
+    st.nshards = n;
+    auto hp = enc->encode_plan();
+    return dev_run(enc, "E", *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+}
+
+static int dev_decode_plan(blbrs_encoder* enc, const uint8_t* present, int data_only,
+                           std::shared_ptr<HostPlan>* hp, std::string* key, bool* nothing) {
+    if (!present) return fail(BLBRS_ERR_INVALID_ARG, "present is NULL");
+    auto pv = present_vec(enc, present);
+    int np = 0;
+    for (uint8_t p : pv) np += p;
+    *nothing = false;
+    if (np == enc->k + enc->m) { *nothing = true; return BLBRS_OK; }
+    if (np < enc->k) return fail(BLBRS_ERR_TOO_FEW_SHARDS, "too few shards given");
+    int rc = BLBRS_OK;
+    *hp = enc->decode_plan(pv, data_only != 0, &rc);
+    if (!*hp) return rc;
+    if ((*hp)->out_idx.empty()) *nothing = true;
+    *key = plan_key(false, pv, data_only != 0);
+    return BLBRS_OK;
+}
+
+int blbrs_reconstruct_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                          size_t batch, size_t shard_len, const uint8_t* present, int data_only, void* stream) {
+    if (!enc) return fail(BLBRS_ERR_INVALID_ARG, "enc is NULL");
+    std::shared_ptr<HostPlan> hp;
+    std::string key;
+    bool nothing = false;
+    int rc = dev_decode_plan(enc, present, data_only, &hp, &key, &nothing);
+    if (rc || nothing || batch == 0 || shard_len == 0) return rc;
+    Stripes st;
+    if ((rc = dev_stripes_strided(enc, stripes, shard_stride, stripe_stride, batch, shard_len, &st))) return rc;
+    return dev_run(enc, key, *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+}
+
+int blbrs_reconstruct_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
+                               const uint8_t* present, int data_only, void* stream) {
+    if (!enc || !shard_ptrs) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    std::shared_ptr<HostPlan> hp;
+    std::string key;
+    bool nothing = false;
+    int rc = dev_decode_plan(enc, present, data_only, &hp, &key, &nothing);
+    if (rc || nothing || batch == 0 || shard_len == 0) return rc;
+    const int n = enc->k + enc->m;
+    PtrLease lease;
+    Stripes st;
+    if ((rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, &st.ptrs, &st.aligned)))
+        return rc;
+    st.nshards = n;
+    return dev_run(enc, key, *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+}
+
+int blbrs_verify_dev(blbrs_encoder* enc, const uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                     size_t batch, size_t shard_len, int32_t* mismatch_dev, void* stream) {
+    if (!enc || !mismatch_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (batch == 0) return BLBRS_OK;
+    HIP_TRY(hipMemsetAsync(mismatch_dev, 0, batch * sizeof(int32_t), static_cast<hipStream_t>(stream)));
+    if (shard_len == 0) return BLBRS_OK;
+    Stripes st;
+    int rc = dev_stripes_strided(enc, const_cast<uint8_t*>(stripes), shard_stride, stripe_stride, batch,
+                                 shard_len, &st);
+    if (rc) return rc;
+    auto hp = enc->encode_plan();
+    return dev_run(enc, "E", *hp, st, batch, shard_len, Mode::kVerify, mismatch_dev, stream);
+}
+
+int blbrs_verify_dev_ptrs(blbrs_encoder* enc, const uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
+                          int32_t* mismatch_dev, void* stream) {
+    if (!enc || !shard_ptrs || !mismatch_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (batch == 0) return BLBRS_OK;
+    HIP_TRY(hipMemsetAsync(mismatch_dev, 0, batch * sizeof(int32_t), static_cast<hipStream_t>(stream)));
+    if (shard_len == 0) return BLBRS_OK;
+    const int n = enc->k + enc->m;
+    PtrLease lease;
+    Stripes st;
+    int rc = upload_ptrs(const_cast<uint8_t* const*>(shard_ptrs), batch * n, static_cast<hipStream_t>(stream),
+                         lease, &st.ptrs, &st.aligned);
+    if (rc) return rc;
+    st.nshards = n;
+    auto hp = enc->encode_plan();
+    return dev_run(enc, "E", *hp, st, batch, shard_len, Mode::kVerify, mismatch_dev, stream);
+}
+
+// ---- streaming host path ----
+
+int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
+                            int nstreams) {
+    if (!enc || !shard_ptrs) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (batch == 0 || shard_len == 0) return BLBRS_OK;
+    const int n = enc->k + enc->m, k = enc->k;
+    for (size_t i = 0; i < batch * n; ++i)
+        if (!shard_ptrs[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
+    if (nstreams < 1) nstreams = 3;
+    if (nstreams > 8) nstreams = 8;
+    int dev = 0;
+    int rc = current_dev_or_fail(&dev);
+    if (rc) return rc;
+    auto hp = enc->encode_plan();
+    const DevPlan* plan = nullptr;
+    if ((rc = enc->dev_plan("E", *hp, dev, &plan))) return rc;
+
+    const size_t Sp = round_up(shard_len, 256);
+    const size_t slot_bytes = static_cast<size_t>(n) * Sp;
+    std::vector<hipStream_t> streams(nstreams, nullptr);
+    uint8_t* dbuf = nullptr;
+    auto cleanup = [&]() {
+        for (auto s : streams)
+            if (s) { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); }
+        if (dbuf) (void)hipFree(dbuf);
+    };
+    for (auto& s : streams) {
+        hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (e != hipSuccess) { cleanup(); return hip_fail(e, "hipStreamCreate"); }
+    }
+    hipError_t e = hipMalloc(&dbuf, slot_bytes * nstreams);
+    if (e != hipSuccess) { dbuf = nullptr; cleanup(); return hip_fail(e, "hipMalloc staging"); }
+    for (size_t b = 0; b < batch && rc == BLBRS_OK; ++b) {
+        const int si = static_cast<int>(b % nstreams);
+        hipStream_t s = streams[si];
+        uint8_t* slot = dbuf + slot_bytes * si;
+        for (int i = 0; i < k && e == hipSuccess; ++i)
+            e = hipMemcpyAsync(slot + i * Sp, shard_ptrs[b * n + i], shard_len, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) { rc = hip_fail(e, "H2D"); break; }
+        Stripes st;
+        st.base = slot;
+        st.shard_stride = Sp;
+        st.stripe_stride = slot_bytes;
+        st.aligned = true;
+        rc = run_plan(*plan, st, 1, shard_len, Mode::kStore, nullptr, s);
+        for (int i = k; i < n && rc == BLBRS_OK && e == hipSuccess; ++i)
+            e = hipMemcpyAsync(shard_ptrs[b * n + i], slot + i * Sp, shard_len, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) rc = hip_fail(e, "D2H");
+    }
+    cleanup();
+    return rc;
+}
+
+// ---- misc ----
+
+int blbrs_set_device(int device) {
+    HIP_TRY(hipSetDevice(device));
+    return BLBRS_OK;
+}
+
+int blbrs_device_count(int* count) {
+    if (!count) return fail(BLBRS_ERR_INVALID_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *count = e == hipSuccess ? n : 0;
+    return BLBRS_OK;
+}
+
+const char* blbrs_last_error(void) { return g_last_error.c_str(); }
+
+const char* blbrs_version(void) { return "blbrs 0.1.0 (gfx950; klauspost/reedsolomon@925cb01d6510 semantics)"; }
+
+const char* blbrs_strerror(int code) {
+    switch (code) {
+        case BLBRS_OK: return "ok";
+        case BLBRS_ERR_INV_SHARD_NUM: return "cannot create Encoder with zero or less data/parity shards";
+        case BLBRS_ERR_MAX_SHARD_NUM: return "cannot create Encoder with more than 256 data+parity shards";
+        case BLBRS_ERR_TOO_FEW_SHARDS: return "too few shards given";
+        case BLBRS_ERR_SHARD_NO_DATA: return "no shard data";
+        case BLBRS_ERR_SHARD_SIZE: return "shard sizes do not match";
+        case BLBRS_ERR_SINGULAR: return "matrix is singular";
+        case BLBRS_ERR_INVALID_ARG: return "invalid argument";
+        case BLBRS_ERR_HIP: return "HIP runtime error";
+        case BLBRS_ERR_NO_DEVICE: return "no HIP device";
+        default: return "unknown error";
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,295 @@
+// rs_kernels.hip -- CDNA4 (gfx950) GF(2^8) Reed-Solomon coding kernels.
+//
+// Replaces klauspost/reedsolomon's codeSomeShards / galMulSlice[Xor] (AVX2 vpshufb nibble
+// tables) that blb runs on the CPU at internal/tractserver/store.go:1099 (Encode),
+// store.go:1133-1136 (Reconstruct + Verify) and client/blb/reconstruct.go:173
+// (ReconstructData).
+//
+// Design (MI355X-first, byte-wise integer work -> HBM-bound, no MFMA):
+//  * A block of 256 threads owns a column tile of one stripe; each lane moves U 16-byte
+//    dwordx4 chunks per shard, so every wave reads k*U coalesced 1 KiB segments and
+//    writes rows*U.  Blocks grid-stride over (stripe, tile), the grid sized to the
+//    resident-block count, so the batch streams through HBM once with nothing re-read.
+//  * GF multiply by a constant uses register lookup tables and v_perm_b32:
+//    byte x = g0 | g1<<3 | g2<<6 (3+3+2 bits) and c*x = T0[g0]^T1[g1]^T2[g2]; each table
+//    has <= 8 one-byte entries, so one v_perm_b32 byte-select over two dwords looks up 4
+//    bytes at once.  Cost: 5 VALU per input dword for the bit groups (shared by every
+//    output row) + 3 perms + 3 xors per (coefficient, dword).  RS(6,3) needs ~23 VALU per
+//    4 input bytes, about a third of the HBM time at full VALU rate: the kernel stays
+//    memory-bound.  LDS log/antilog lookups would need k*m ds_read_u8 per byte with random
+//    bank conflicts and cap well below the roofline (SURVEY.md §7 "Hard parts").
+//  * Coefficient tables (5 dwords per coefficient) are wave-uniform and re-read with
+//    scalar loads each tile (scalar-cache hits) instead of being pinned for the whole
+//    launch, which would overflow the SGPR file and spill through v_writelane/readlane.
+//  * Every output byte is written, never accumulated into: callers hand in un-zeroed
+//    pooled buffers (pkg/rpc/pool.go:28-43).
+//  * A tile that is not entirely inside the shard (length not a multiple of the tile) or
+//    whose shards are not 16-byte aligned takes a byte-wise path; results are identical by
+//    construction because byte columns are independent.
+#include "rs_kernels.hpp"
+
+namespace blbrs {
+namespace {
+
+struct alignas(16) V4 { uint32_t x, y, z, w; };
+
+// Read-only metadata (tables, shard indices, pointer tables) is read through the constant
+// address space so the compiler may use scalar (s_load) loads for it.
+using cu32 = const uint32_t __attribute__((address_space(4)))*;
+using ci32 = const int32_t __attribute__((address_space(4)))*;
+using cu64 = const uint64_t __attribute__((address_space(4)))*;
+__device__ __forceinline__ cu32 as_const(const uint32_t* p) { return (cu32)(uintptr_t)p; }
+__device__ __forceinline__ ci32 as_const(const int32_t* p) { return (ci32)(uintptr_t)p; }
+__device__ __forceinline__ cu64 as_const(const uint64_t* p) { return (cu64)(uintptr_t)p; }
+
+template <typename TP>
+__device__ __forceinline__ uint32_t gmul(TP t, uint32_t g0, uint32_t g1, uint32_t g2) {
+    return __builtin_amdgcn_perm(t[1], t[0], g0) ^ __builtin_amdgcn_perm(t[3], t[2], g1) ^
+           __builtin_amdgcn_perm(0u, t[4], g2);
+}
+
+// acc[r] ^= coef(r, c) * x over NV input dwords of ONE input shard c.  Bit groups are
+// split once per dword and shared by every row; each row's 5 table words are fetched once
+// and applied to all NV dwords (amortises the SGPR->VGPR moves v_perm needs for its
+// second table operand under gfx9's one-SGPR constant-bus limit).
+template <int MR, int NV, typename Tab>
+__device__ __forceinline__ void madd(const uint32_t (&x)[NV], Tab tab, uint32_t (&acc)[MR][NV], int nr) {
+    uint32_t g0[NV], g1[NV], g2[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        g0[v] = x[v] & 0x07070707u;
+        g1[v] = (x[v] >> 3) & 0x07070707u;
+        g2[v] = (x[v] >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+        if (r < nr) {
+            const auto tp = tab(r);
+            const uint32_t t[5] = {tp[0], tp[1], tp[2], tp[3], tp[4]};
+#pragma unroll
+            for (int v = 0; v < NV; ++v) acc[r][v] ^= gmul(t, g0[v], g1[v], g2[v]);
+        }
+    }
+}
+
+__device__ __forceinline__ void unpack(const V4& q, uint32_t* w) { w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w; }
+__device__ __forceinline__ V4 pack(const uint32_t* w) { return V4{w[0], w[1], w[2], w[3]}; }
+
+template <int ADDR>
+__device__ __forceinline__ uint8_t* shard_ptr(const CodeArgs& a, uint32_t b, int idx) {
+    if constexpr (ADDR == 0)
+        return a.base + static_cast<uint64_t>(b) * a.stripe_stride +
+               static_cast<uint64_t>(idx) * a.shard_stride;
+    else
+        return reinterpret_cast<uint8_t*>(as_const(a.ptrs)[static_cast<uint64_t>(b) * a.nshards + idx]);
+}
+
+__device__ __forceinline__ V4 load_bytes(const uint8_t* p, uint32_t n) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t j = 0; j < n; ++j) w[j >> 2] |= static_cast<uint32_t>(p[j]) << (8 * (j & 3));
+    return V4{w[0], w[1], w[2], w[3]};
+}
+
+__device__ __forceinline__ void store_bytes(uint8_t* p, const V4& v, uint32_t n) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t j = 0; j < n; ++j) p[j] = static_cast<uint8_t>(w[j >> 2] >> (8 * (j & 3)));
+}
+
+__device__ __forceinline__ bool neq(const V4& a, const V4& b) {
+    return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) != 0u;
+}
+
+// Byte-wise path for partial / unaligned tiles (runtime k, rows <= MR).
+template <int MR, int MODE, int ADDR, int U>
+__device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, uint64_t tile_off) {
+    const int nr = a.rows;
+    for (int u = 0; u < U; ++u) {
+        const uint64_t off = tile_off + (static_cast<uint64_t>(u) * kThreads + threadIdx.x) * kBytesPerThread;
+        if (off >= a.S) return;
+        const uint32_t nb = static_cast<uint32_t>(a.S - off < 16 ? a.S - off : 16);
+        uint32_t acc[MR][4] = {};
+        for (int c = 0; c < a.k; ++c) {
+            uint32_t x[4];
+            unpack(load_bytes(shard_ptr<ADDR>(a, b, as_const(a.in_idx)[c]) + off, nb), x);
+            madd<MR, 4>(x, [&](int r) { return as_const(a.tables) + (static_cast<uint32_t>(r) * a.k + c) * 5; },
+                        acc, nr);
+        }
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            if (r >= nr) break;
+            uint8_t* q = shard_ptr<ADDR>(a, b, as_const(a.out_idx)[r]) + off;
+            if constexpr (MODE == 0) store_bytes(q, pack(acc[r]), nb);
+            else if (neq(load_bytes(q, nb), pack(acc[r]))) atomicOr(&a.mismatch[b], 1);
+        }
+    }
+}
+
+// K > 0: compile-time input count (all K*U chunk loads issued before any math).
+// K == 0: runtime k (loads issued per input, two inputs unrolled).
+// MR: compile-time bound on output rows; a.rows <= MR honoured at runtime.
+// MODE 0 = store outputs, 1 = compare against existing outputs (Verify).
+// ADDR 0 = strided stripes, 1 = pointer table.  U = 16-byte chunks per lane per tile.
+template <int K, int MR, int MODE, int ADDR, int U>
+__global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
+    constexpr uint32_t kTile = kTileBytes * U;
+    const uint32_t total = a.B * a.tiles_per_stripe;
+    const int nr = a.rows;
+    const bool aligned = a.aligned != 0;
+
+    for (uint32_t t = blockIdx.x; t < total; t += gridDim.x) {
+        const uint32_t b = t / a.tiles_per_stripe;
+        const uint64_t tile_off = static_cast<uint64_t>(t - b * a.tiles_per_stripe) * kTile;
+        if (!aligned || tile_off + kTile > a.S) {
+            code_tile_slow<MR, MODE, ADDR, U>(a, b, tile_off);
+            continue;
+        }
+        // Opaque per-iteration copy of the table pointer: keeps the scalar table loads
+        // inside the loop (no LICM -> no SGPR spill of K*MR*5 words).
+        cu32 tables = as_const(a.tables);
+        asm volatile("" : "+s"(tables));
+        const ci32 in_idx = as_const(a.in_idx);
+        const ci32 out_idx = as_const(a.out_idx);
+        const uint64_t lane_off = tile_off + static_cast<uint64_t>(threadIdx.x) * kBytesPerThread;
+
+        constexpr int NV = 4 * U;           // input dwords per lane per shard
+        constexpr uint32_t kStep = kThreads * kBytesPerThread;
+        uint32_t acc[MR][NV] = {};
+
+        if constexpr (K > 0) {
+            V4 x[K][U];
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[c][u] = *reinterpret_cast<const V4*>(p + u * kStep);
+            }
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                uint32_t xv[NV];
+#pragma unroll
+                for (int u = 0; u < U; ++u) unpack(x[c][u], xv + 4 * u);
+                madd<MR, NV>(xv, [&](int r) { return tables + (r * K + c) * 5; }, acc, nr);
+            }
+        } else {
+            const int k = a.k;
+#pragma unroll 2
+            for (int c = 0; c < k; ++c) {
+                const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
+                uint32_t xv[NV];
+#pragma unroll
+                for (int u = 0; u < U; ++u) unpack(*reinterpret_cast<const V4*>(p + u * kStep), xv + 4 * u);
+                madd<MR, NV>(xv, [&](int r) { return tables + (static_cast<uint32_t>(r) * k + c) * 5; }, acc, nr);
+            }
+        }
+
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            if (r >= nr) break;
+            uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
+            if constexpr (MODE == 0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) *reinterpret_cast<V4*>(q + u * kStep) = pack(acc[r] + 4 * u);
+            } else {
+                bool bad = false;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    bad |= neq(*reinterpret_cast<const V4*>(q + u * kStep), pack(acc[r] + 4 * u));
+                if (bad) atomicOr(&a.mismatch[b], 1);
+            }
+        }
+    }
+}
+
+using KernelFn = void (*)(CodeArgs);
+
+// Compile-time input counts: blb's classes RS(6,3), RS(8,3), RS(10,3), RS(12,5)
+// (internal/core/StorageClass.go:7-13), the bench's RS(10,4), the reference tests' RS(3,2)
+// (store_test.go:750,818) and RS(4,2); rows 1..5 cover every encode and decode of those.
+#define BLBRS_K_LIST(X) X(3) X(4) X(6) X(8) X(10) X(12)
+constexpr int kMaxTemplRows = 5;
+
+template <int K, int MODE, int ADDR, int U>
+KernelFn pick_rows(int rows) {
+    constexpr bool kGeneric = K == 0;
+    switch (rows) {
+        case 1: return rs_code_kernel<K, 1, MODE, ADDR, U>;
+        case 2: return rs_code_kernel<K, 2, MODE, ADDR, U>;
+        case 3: return rs_code_kernel<K, 3, MODE, ADDR, U>;
+        case 4: return rs_code_kernel<K, 4, MODE, ADDR, U>;
+        case 5: return rs_code_kernel<K, 5, MODE, ADDR, U>;
+        case 6: return kGeneric ? rs_code_kernel<0, 6, MODE, ADDR, U> : nullptr;
+        case 7: return kGeneric ? rs_code_kernel<0, 7, MODE, ADDR, U> : nullptr;
+        case 8: return kGeneric ? rs_code_kernel<0, 8, MODE, ADDR, U> : nullptr;
+        default: return nullptr;
+    }
+}
+
+template <int MODE, int ADDR, int U>
+KernelFn pick_k(int k, int rows, bool* fixed) {
+    *fixed = true;
+    if (rows <= kMaxTemplRows) {
+        switch (k) {
+#define BLBRS_CASE(KK) case KK: return pick_rows<KK, MODE, ADDR, U>(rows);
+            BLBRS_K_LIST(BLBRS_CASE)
+#undef BLBRS_CASE
+            default: break;
+        }
+    }
+    *fixed = false;
+    return pick_rows<0, MODE, ADDR, U>(rows);
+}
+
+constexpr int kU = 2;  // chunks per lane per tile (8 KiB column tiles)
+
+KernelFn pick(int k, int rows, Mode mode, bool strided, bool* fixed) {
+    if (mode == Mode::kStore)
+        return strided ? pick_k<0, 0, kU>(k, rows, fixed) : pick_k<0, 1, kU>(k, rows, fixed);
+    return strided ? pick_k<1, 0, kU>(k, rows, fixed) : pick_k<1, 1, kU>(k, rows, fixed);
+}
+
+int blocks_per_cu(KernelFn fn) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), kThreads, 0) !=
+            hipSuccess || n <= 0)
+        n = 4;
+    return n;
+}
+
+int cu_count() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+    return n;
+}
+
+}  // namespace
+
+uint32_t tile_bytes() { return static_cast<uint32_t>(kTileBytes) * kU; }
+
+hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream) {
+    if (args.rows < 1 || args.rows > kMaxRows || args.k < 1) return hipErrorInvalidValue;
+    if (args.B == 0 || args.S == 0) return hipSuccess;
+    bool fixed = false;
+    KernelFn fn = pick(args.k, args.rows, mode, args.base != nullptr, &fixed);
+    if (!fn) return hipErrorInvalidValue;
+    // Resident-grid sizing: blocks grid-stride over (stripe, tile); CUs x resident blocks
+    // keeps all 256 CUs streaming with no tail wave of late blocks.
+    static thread_local KernelFn last_fn = nullptr;
+    static thread_local int last_bpc = 0, last_cus = 0;
+    if (fn != last_fn) { last_bpc = blocks_per_cu(fn); last_cus = cu_count(); last_fn = fn; }
+    const uint64_t total = static_cast<uint64_t>(args.B) * args.tiles_per_stripe;
+    uint64_t grid = static_cast<uint64_t>(last_cus) * static_cast<uint64_t>(last_bpc);
+    if (grid > total) grid = total;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream, args);
+    return hipGetLastError();
+}
+
+const char* kernel_name(int k, int rows, Mode mode) {
+    bool fixed = false;
+    pick(k, rows, mode, true, &fixed);
+    return fixed ? "rs_code_kernel<K,MR,MODE,ADDR,U>" : "rs_code_kernel<0,MR,MODE,ADDR,U>";
+}
+
+}  // namespace blbrs

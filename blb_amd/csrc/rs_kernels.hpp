@@ -1,0 +1,46 @@
+// rs_kernels.hpp -- launch interface of the GF(2^8) coding kernels (rs_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace blbrs {
+
+// One coding pass: out[r] = XOR_c coef[r][c] * in[c] over every byte column of every
+// stripe in the batch.  The same kernel serves Encode (rows = parity rows of M),
+// Reconstruct[Data] (rows = inv(M[valid]) and P*inv(M[valid])) and Verify (rows = parity
+// rows, outputs compared instead of stored).
+struct CodeArgs {
+    const uint32_t* tables;   // device: [rows][k][5] v_perm lookup words (gf256.hpp)
+    const int32_t* in_idx;    // device: [k] shard index (within a stripe) of input c
+    const int32_t* out_idx;   // device: [rows] shard index of output r
+    uint8_t* base;            // strided addressing when non-null
+    uint64_t shard_stride;    //   shard i of stripe b at base + b*stripe_stride + i*shard_stride
+    uint64_t stripe_stride;
+    const uint64_t* ptrs;     // pointer-table addressing when base == null: [B][nshards]
+    uint32_t nshards;         //   k+m entries per stripe
+    uint32_t B;               // stripes in the batch
+    uint64_t S;               // shard length in bytes
+    uint32_t tiles_per_stripe;
+    int32_t k;                // inputs per stripe
+    int32_t rows;             // outputs per stripe (<= kMaxRows)
+    int32_t aligned;          // every shard address 16-byte aligned (vector path allowed)
+    int32_t* mismatch;        // verify: [B] flags (device)
+};
+
+constexpr int kThreads = 256;
+constexpr int kBytesPerThread = 16;                       // one dwordx4 per shard per lane
+constexpr int kTileBytes = kThreads * kBytesPerThread;    // byte columns per block-iteration
+constexpr int kMaxRows = 8;                               // outputs per pass
+
+enum class Mode : int { kStore = 0, kVerify = 1 };
+
+// Launches one pass on `stream`; returns hipSuccess or the launch error.
+hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream);
+
+// Name of the kernel instantiation launch_code() would pick (for profiling/tests).
+const char* kernel_name(int k, int rows, Mode mode);
+
+// Column bytes one block-iteration covers; CodeArgs::tiles_per_stripe = ceil(S / this).
+uint32_t tile_bytes();
+
+}  // namespace blbrs

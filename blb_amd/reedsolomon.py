@@ -1,0 +1,321 @@
+"""Host-side mirror of github.com/klauspost/reedsolomon's Encoder (the interface blb binds),
+running on the MI355X engine through the C ABI in include/blb_rs.h.
+
+Same names, argument meaning and error behaviour as the Go library at the pinned version
+(/root/reference/go.mod:20), so that the parity tests read like blb's own tests:
+
+    enc = reedsolomon.New(n, m)          # internal/tractserver/store.go:1022
+    enc.Encode(shards)                   # store.go:1099
+    enc.Reconstruct(shards)              # store.go:1133   (reconstructAndVerify)
+    ok = enc.Verify(shards)              # store.go:1136
+    enc.ReconstructData(shards)          # client/blb/reconstruct.go:173
+
+`shards` is a list of k+m shards, data first.  A shard is a 1-D C-contiguous numpy uint8
+array (host memory: copied through the GPU) or a 1-D torch.uint8 CUDA tensor (device
+memory: coded in place on the current torch stream).  For Reconstruct*, a missing shard
+is None or empty; like klauspost's `make`, a fresh buffer is allocated and stored back into
+the list, unless `outs={index: buffer}` supplies one (klauspost reuses cap >= size --
+the client's `thisB[0:0:length]` trick at client/blb/reconstruct.go:172-175).
+
+Batched device-resident methods (EncodeBatch / ReconstructBatch / VerifyBatch) take a
+torch.uint8 CUDA tensor [B, k+m, S] of stripes -- the bench / batched-caller path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+
+class RSError(Exception):
+    """Base of the klauspost error values."""
+    code = 0
+
+
+class ErrInvShardNum(RSError):
+    code = -1
+
+
+class ErrMaxShardNum(RSError):
+    code = -2
+
+
+class ErrTooFewShards(RSError):
+    code = -3
+
+
+class ErrShardNoData(RSError):
+    code = -4
+
+
+class ErrShardSize(RSError):
+    code = -5
+
+
+class ErrSingular(RSError):
+    code = -6
+
+
+class ErrInvalidArgument(RSError):
+    code = -7
+
+
+class ErrHIP(RSError):
+    code = -8
+
+
+class ErrNoDevice(RSError):
+    code = -9
+
+
+_ERRORS = {c.code: c for c in (ErrInvShardNum, ErrMaxShardNum, ErrTooFewShards, ErrShardNoData,
+                                ErrShardSize, ErrSingular, ErrInvalidArgument, ErrHIP, ErrNoDevice)}
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        lib = _lib.load()
+        msg = lib.blbrs_last_error().decode() or lib.blbrs_strerror(rc).decode()
+        raise _ERRORS.get(rc, RSError)(msg)
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _torch_stream(dev_tensor) -> int:
+    import torch
+    return torch.cuda.current_stream(dev_tensor.device).cuda_stream
+
+
+def _shard_len(s) -> int:
+    if s is None:
+        return 0
+    return int(s.numel()) if _is_torch(s) else int(s.size)
+
+
+def _host_ptr(a: np.ndarray) -> int:
+    if not isinstance(a, np.ndarray) or a.dtype != np.uint8 or a.ndim != 1 or not a.flags.c_contiguous:
+        raise ErrInvalidArgument("host shards must be 1-D C-contiguous numpy uint8 arrays")
+    return a.ctypes.data
+
+
+def _dev_ptr(t) -> int:
+    import torch
+    if t.dtype != torch.uint8 or t.dim() != 1 or not t.is_cuda or (t.numel() > 1 and t.stride(0) != 1):
+        raise ErrInvalidArgument("device shards must be 1-D contiguous torch.uint8 CUDA tensors")
+    return t.data_ptr()
+
+
+class Encoder:
+    """reedsolomon.Encoder for (DataShards, ParityShards), backed by libblbrs."""
+
+    def __init__(self, data_shards: int, parity_shards: int):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        _check(self._lib.blbrs_new(int(data_shards), int(parity_shards), ctypes.byref(h)))
+        self._h = h
+        self.DataShards = int(data_shards)
+        self.ParityShards = int(parity_shards)
+        self.Shards = self.DataShards + self.ParityShards
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.blbrs_free(h)
+            self._h = None
+
+    # ---- introspection ----
+    def matrix(self) -> np.ndarray:
+        out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
+        _check(self._lib.blbrs_matrix(self._h, out.ctypes.data, out.size))
+        return out
+
+    # ---- helpers ----
+    def _arrays(self, shards, n):
+        ptrs = (ctypes.c_void_p * n)()
+        lens = (ctypes.c_size_t * n)()
+        return ptrs, lens
+
+    def _kind(self, shards) -> Optional[str]:
+        kinds = {("dev" if _is_torch(s) else "host") for s in shards if _shard_len(s)}
+        if len(kinds) > 1:
+            raise ErrInvalidArgument("mixing host and device shards in one call")
+        return kinds.pop() if kinds else None
+
+    @staticmethod
+    def _check_sizes(lens: Sequence[int], nilok: bool) -> int:
+        """reedsolomon.go checkShards / shardSize."""
+        size = next((x for x in lens if x), 0)
+        if size == 0:
+            raise ErrShardNoData("no shard data")
+        for x in lens:
+            if x != size and (x != 0 or not nilok):
+                raise ErrShardSize("shard sizes do not match")
+        return size
+
+    # ---- Encoder interface ----
+    def Encode(self, shards: list) -> None:
+        """Encode parity for shards[0:k] into shards[k:k+m] (fully overwritten)."""
+        n = self.Shards
+        if len(shards) != n:
+            raise ErrTooFewShards("too few shards given")
+        lens = [_shard_len(s) for s in shards]
+        self._check_sizes(lens, nilok=False)
+        if self._kind(shards) == "dev":
+            ptrs = (ctypes.c_void_p * n)(*[_dev_ptr(s) for s in shards])
+            _check(self._lib.blbrs_encode_dev_ptrs(self._h, ptrs, 1, lens[0], _torch_stream(shards[0])))
+            return
+        ptrs = (ctypes.c_void_p * n)(*[_host_ptr(s) for s in shards])
+        L = (ctypes.c_size_t * n)(*lens)
+        _check(self._lib.blbrs_encode(self._h, ptrs, L))
+
+    def Verify(self, shards: list) -> bool:
+        """True when the parity shards equal the encoding of the data shards."""
+        n = self.Shards
+        if len(shards) != n:
+            raise ErrTooFewShards("too few shards given")
+        lens = [_shard_len(s) for s in shards]
+        self._check_sizes(lens, nilok=False)
+        if self._kind(shards) == "dev":
+            import torch
+            flag = torch.empty(1, dtype=torch.int32, device=shards[0].device)
+            ptrs = (ctypes.c_void_p * n)(*[_dev_ptr(s) for s in shards])
+            _check(self._lib.blbrs_verify_dev_ptrs(self._h, ptrs, 1, lens[0], flag.data_ptr(),
+                                                    _torch_stream(shards[0])))
+            return int(flag.item()) == 0
+        ptrs = (ctypes.c_void_p * n)(*[_host_ptr(s) for s in shards])
+        L = (ctypes.c_size_t * n)(*lens)
+        ok = ctypes.c_int(0)
+        _check(self._lib.blbrs_verify(self._h, ptrs, L, ctypes.byref(ok)))
+        return bool(ok.value)
+
+    def _reconstruct(self, shards: list, data_only: bool, outs: Optional[dict]) -> None:
+        n = self.Shards
+        if len(shards) != n:
+            raise ErrTooFewShards("too few shards given")
+        lens = [_shard_len(s) for s in shards]
+        size = self._check_sizes(lens, nilok=True)
+        present = [x != 0 for x in lens]
+        if all(present):
+            return
+        if sum(present) < self.DataShards:
+            raise ErrTooFewShards("too few shards given")
+        kind = self._kind(shards)
+        outs = outs or {}
+        produce = [i for i in range(n) if not present[i] and (i < self.DataShards or not data_only)]
+        bufs = list(shards)
+        for i in produce:
+            if i in outs:
+                o = outs[i]
+                if _shard_len(o) < size:
+                    raise ErrInvalidArgument(f"output buffer for shard {i} is smaller than the shard size")
+                bufs[i] = o[:size]
+            elif kind == "dev":
+                import torch
+                ref = next(s for s in shards if _shard_len(s))
+                bufs[i] = torch.empty(size, dtype=torch.uint8, device=ref.device)
+            else:
+                bufs[i] = np.empty(size, dtype=np.uint8)
+        if kind == "dev":
+            ptrs = (ctypes.c_void_p * n)(*[_dev_ptr(bufs[i]) if (present[i] or i in produce) else None
+                                           for i in range(n)])
+            pres = (ctypes.c_uint8 * n)(*[1 if p else 0 for p in present])
+            ref = next(s for s in shards if _shard_len(s))
+            _check(self._lib.blbrs_reconstruct_dev_ptrs(self._h, ptrs, 1, size, pres, int(data_only),
+                                                         _torch_stream(ref)))
+        else:
+            ptrs = (ctypes.c_void_p * n)(*[_host_ptr(bufs[i]) if (present[i] or i in produce) else None
+                                           for i in range(n)])
+            L = (ctypes.c_size_t * n)(*lens)
+            fn = self._lib.blbrs_reconstruct_data if data_only else self._lib.blbrs_reconstruct
+            _check(fn(self._h, ptrs, L))
+        for i in produce:
+            shards[i] = bufs[i]
+
+    def Reconstruct(self, shards: list, outs: Optional[dict] = None) -> None:
+        """Rebuild every missing shard (data and parity) in the list."""
+        self._reconstruct(shards, False, outs)
+
+    def ReconstructData(self, shards: list, outs: Optional[dict] = None) -> None:
+        """Rebuild missing data shards only; parity slots stay missing."""
+        self._reconstruct(shards, True, outs)
+
+    # ---- batched device-resident path ----
+    def _stripes(self, stripes):
+        import torch
+        if not (_is_torch(stripes) and stripes.is_cuda and stripes.dtype == torch.uint8 and stripes.dim() == 3):
+            raise ErrInvalidArgument("stripes must be a [B, k+m, S] torch.uint8 CUDA tensor")
+        B, n, S = stripes.shape
+        if n != self.Shards:
+            raise ErrTooFewShards("too few shards given")
+        if S > 1 and stripes.stride(2) != 1:
+            raise ErrInvalidArgument("shard bytes must be contiguous (stride(2) == 1)")
+        return B, S, stripes.stride(1), stripes.stride(0)
+
+    def EncodeBatch(self, stripes, stream: Optional[int] = None) -> None:
+        """Encode every stripe of a [B, k+m, S] device tensor in place (async on the stream)."""
+        B, S, ss, bs = self._stripes(stripes)
+        st = _torch_stream(stripes) if stream is None else stream
+        _check(self._lib.blbrs_encode_dev(self._h, stripes.data_ptr(), ss, bs, B, S, st))
+
+    def ReconstructBatch(self, stripes, present: Sequence[bool], data_only: bool = False,
+                         stream: Optional[int] = None) -> None:
+        """Rebuild the shards marked absent in `present` for every stripe, in place."""
+        B, S, ss, bs = self._stripes(stripes)
+        if len(present) != self.Shards:
+            raise ErrTooFewShards("too few shards given")
+        pres = (ctypes.c_uint8 * self.Shards)(*[1 if p else 0 for p in present])
+        st = _torch_stream(stripes) if stream is None else stream
+        _check(self._lib.blbrs_reconstruct_dev(self._h, stripes.data_ptr(), ss, bs, B, S, pres,
+                                               int(data_only), st))
+
+    def VerifyBatch(self, stripes, stream: Optional[int] = None):
+        """Returns a [B] torch.bool CUDA tensor: True where the stripe's parity is consistent."""
+        import torch
+        B, S, ss, bs = self._stripes(stripes)
+        flags = torch.empty(B, dtype=torch.int32, device=stripes.device)
+        st = _torch_stream(stripes) if stream is None else stream
+        _check(self._lib.blbrs_verify_dev(self._h, stripes.data_ptr(), ss, bs, B, S, flags.data_ptr(), st))
+        return flags == 0
+
+    def EncodeHostBatch(self, stripes: Sequence[Sequence[np.ndarray]], nstreams: int = 3) -> None:
+        """Streaming encode of host-resident stripes (pinned memory gives full PCIe rate)."""
+        n = self.Shards
+        B = len(stripes)
+        if B == 0:
+            return
+        S = _shard_len(stripes[0][0])
+        flat = []
+        for st in stripes:
+            if len(st) != n:
+                raise ErrTooFewShards("too few shards given")
+            for s in st:
+                if _shard_len(s) != S:
+                    raise ErrShardSize("shard sizes do not match")
+                flat.append(_host_ptr(s))
+        ptrs = (ctypes.c_void_p * len(flat))(*flat)
+        _check(self._lib.blbrs_encode_host_batch(self._h, ptrs, B, S, int(nstreams)))
+
+
+def New(data_shards: int, parity_shards: int) -> Encoder:
+    """reedsolomon.New(dataShards, parityShards) -> Encoder (raises ErrInvShardNum /
+    ErrMaxShardNum like the Go constructor)."""
+    return Encoder(data_shards, parity_shards)
+
+
+def set_device(device: int) -> None:
+    _check(_lib.load().blbrs_set_device(int(device)))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(_lib.load().blbrs_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def version() -> str:
+    return _lib.load().blbrs_version().decode()

@@ -1,0 +1,134 @@
+/*
+ * blb_rs.h -- C ABI of the MI355X Reed-Solomon engine (libblbrs.so).
+ *
+ * Drop-in boundary for blb's use of github.com/klauspost/reedsolomon
+ * (@925cb01d6510, /root/reference/go.mod:20).  blb binds exactly four methods of the Go
+ * interface reedsolomon.Encoder plus the constructor:
+ *
+ *   reedsolomon.New(n, m)        internal/tractserver/store.go:1022, client/blb/reconstruct.go:166
+ *   Encoder.Encode(shards)       internal/tractserver/store.go:1099
+ *   Encoder.Reconstruct(shards)  internal/tractserver/store.go:1133
+ *   Encoder.Verify(shards)       internal/tractserver/store.go:1136
+ *   Encoder.ReconstructData(s)   client/blb/reconstruct.go:173
+ *
+ * Each of those has a host-memory entry point below with the same argument meaning and
+ * error behaviour; a cgo shim marshals Go's [][]byte into the
+ * (pointer, length) arrays.  The *_dev entry points are the device-resident batched path
+ * used when stripes already live in HBM (bench.py, batched callers).
+ *
+ * Conventions (klauspost semantics, reproduced exactly):
+ *   - shards[] / lens[] always have k+m entries, data shards first.
+ *   - A shard with lens[i] == 0 is "missing" (Reconstruct*) -- its pointer must then be a
+ *     caller buffer with room for the shard size (klauspost reslices shards[i][0:size] when
+ *     cap >= size; client/blb/reconstruct.go:172-175 relies on the output landing in the
+ *     caller's buffer), or NULL for a parity slot that ReconstructData will not produce.
+ *   - Outputs are fully overwritten, never accumulated into (rpc.GetBuffer returns
+ *     un-zeroed pooled buffers, pkg/rpc/pool.go:28-43).
+ *   - No pointer is retained after a call returns (cgo rule).
+ *   - All functions are thread-safe; each host-memory call picks a stream worker on the
+ *     calling thread's current HIP device (blbrs_set_device()).
+ */
+#ifndef BLB_RS_H
+#define BLB_RS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes: 1:1 with klauspost's exported errors (reedsolomon.go), plus engine errors. */
+#define BLBRS_OK                 0
+#define BLBRS_ERR_INV_SHARD_NUM (-1) /* ErrInvShardNum: "cannot create Encoder with zero or less data/parity shards" */
+#define BLBRS_ERR_MAX_SHARD_NUM (-2) /* ErrMaxShardNum: "cannot create Encoder with more than 256 data+parity shards" */
+#define BLBRS_ERR_TOO_FEW_SHARDS (-3) /* ErrTooFewShards: "too few shards given" */
+#define BLBRS_ERR_SHARD_NO_DATA (-4) /* ErrShardNoData: "no shard data" */
+#define BLBRS_ERR_SHARD_SIZE    (-5) /* ErrShardSize: "shard sizes do not match" */
+#define BLBRS_ERR_SINGULAR      (-6) /* errSingular (matrix.go): "matrix is singular" */
+#define BLBRS_ERR_INVALID_ARG   (-7) /* NULL pointer / bad stride / missing output buffer */
+#define BLBRS_ERR_HIP           (-8) /* HIP runtime failure; see blbrs_last_error() */
+#define BLBRS_ERR_NO_DEVICE     (-9) /* no gfx950 device visible */
+
+typedef struct blbrs_encoder blbrs_encoder;
+
+/* ---- construction (reedsolomon.New) ---- */
+
+/* reedsolomon.New(dataShards, parityShards): builds the (k+m) x k systematic matrix
+ * M = V * inv(V[0:k]), V[r][c] = r^c over GF(2^8)/0x11D.  Errors: INV_SHARD_NUM when
+ * k <= 0 or m <= 0, MAX_SHARD_NUM when k + m > 256. */
+int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out);
+void blbrs_free(blbrs_encoder* enc);
+int blbrs_data_shards(const blbrs_encoder* enc);
+int blbrs_parity_shards(const blbrs_encoder* enc);
+/* Copies the (k+m)*k encoding matrix (row-major) into out; cap must be >= (k+m)*k. */
+int blbrs_matrix(const blbrs_encoder* enc, uint8_t* out, size_t cap);
+
+/* ---- host-memory Encoder methods (what the cgo shim binds) ---- */
+
+/* Encoder.Encode: shards[0..k) in, shards[k..k+m) out.  All k+m lens equal and non-zero
+ * (else SHARD_NO_DATA / SHARD_SIZE). */
+int blbrs_encode(blbrs_encoder* enc, uint8_t* const* shards, const size_t* lens);
+
+/* Encoder.Verify: *ok = 1 when the parity shards equal P * data, 0 otherwise
+ * (klauspost returns (false, nil) on mismatch). */
+int blbrs_verify(blbrs_encoder* enc, const uint8_t* const* shards, const size_t* lens, int* ok);
+
+/* Encoder.Reconstruct: rebuild every missing shard (data and parity).  lens[i] is set to
+ * the shard size for every slot produced.  All present: no work, OK.  Fewer than k
+ * present: TOO_FEW_SHARDS.  Decode uses the first k present indices ascending. */
+int blbrs_reconstruct(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens);
+
+/* Encoder.ReconstructData: rebuild missing data shards only; parity slots untouched. */
+int blbrs_reconstruct_data(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens);
+
+/* ---- device-resident batched path (stripes already in HBM) ----
+ * Strided layout: shard i of stripe b lives at
+ *     stripes + b * stripe_stride + i * shard_stride          (i in [0, k+m))
+ * The *_ptrs forms take a HOST array of batch*(k+m) DEVICE pointers, stripe-major.
+ * stream is a hipStream_t (NULL = default stream); calls are asynchronous on it.
+ * Device: the calling thread's current HIP device. */
+
+/* Batched Encode: parity shards k..k+m-1 of every stripe are (over)written. */
+int blbrs_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
+                     size_t stripe_stride, size_t batch, size_t shard_len, void* stream);
+int blbrs_encode_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch,
+                          size_t shard_len, void* stream);
+
+/* Batched Reconstruct / ReconstructData with ONE erasure pattern for the whole batch
+ * (present[i] != 0 means shard i is intact in every stripe).  Missing data shards (and,
+ * unless data_only, missing parity shards) are written in place.  All rows are produced
+ * in a single pass over the k surviving shards (missing parity uses P * inv(M[valid])). */
+int blbrs_reconstruct_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
+                          size_t stripe_stride, size_t batch, size_t shard_len,
+                          const uint8_t* present, int data_only, void* stream);
+int blbrs_reconstruct_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch,
+                               size_t shard_len, const uint8_t* present, int data_only,
+                               void* stream);
+
+/* Batched Verify: mismatch_dev is a DEVICE int32 array of batch entries; entry b is set
+ * to 1 when stripe b's parity differs from P * data (entries are zeroed first). */
+int blbrs_verify_dev(blbrs_encoder* enc, const uint8_t* stripes, size_t shard_stride,
+                     size_t stripe_stride, size_t batch, size_t shard_len,
+                     int32_t* mismatch_dev, void* stream);
+int blbrs_verify_dev_ptrs(blbrs_encoder* enc, const uint8_t* const* shard_ptrs, size_t batch,
+                          size_t shard_len, int32_t* mismatch_dev, void* stream);
+
+/* ---- streaming host path (pinned host stripes -> GPU -> pinned host parity) ----
+ * Encodes `batch` stripes whose k+m shards are HOST pointers (shard_ptrs stripe-major),
+ * overlapping H2D copies, kernels and D2H copies over `nstreams` streams on the calling
+ * thread's device.  Pinned (hipHostMalloc / hipHostRegister) buffers give full PCIe rate. */
+int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch,
+                            size_t shard_len, int nstreams);
+
+/* ---- misc ---- */
+int blbrs_set_device(int device);      /* hipSetDevice for the calling thread */
+int blbrs_device_count(int* count);
+const char* blbrs_last_error(void);    /* thread-local message for the last failure */
+const char* blbrs_version(void);
+const char* blbrs_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLB_RS_H */

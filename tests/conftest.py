@@ -1,0 +1,33 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libblbrs.so on the GPU)")
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    from oracle import oracle as O
+    O.build()
+    return O
+
+
+@pytest.fixture(scope="session")
+def golden():
+    """All committed golden fixtures, keyed by (k, m)."""
+    import numpy as np
+    out = {}
+    gdir = os.path.join(ROOT, "tests", "golden")
+    for fn in sorted(os.listdir(gdir)):
+        if fn.endswith(".npz"):
+            z = np.load(os.path.join(gdir, fn))  # allow_pickle=False (default)
+            d = {key: z[key] for key in z.files}
+            out[(int(d["k"]), int(d["m"]))] = d
+    return out

@@ -1,0 +1,108 @@
+"""CPU-side tests of the C ABI (no compute calls need a GPU here):
+  * libblbrs.so loads and exports every function include/blb_rs.h declares;
+  * reedsolomon.New's argument errors and the encoding matrix match the oracle;
+  * without a GPU the engine fails loudly (ErrNoDevice) -- there is no CPU fallback.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "blb_rs.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(blbrs_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from blb_amd import _lib
+    lib = _lib.load()
+    declared = header_functions()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(lib, name), f"libblbrs.so does not export {name}"
+        assert name in _lib.SIGNATURES, f"ctypes signature missing for {name}"
+    assert set(_lib.SIGNATURES) == set(declared)
+
+
+def test_error_codes_match_header():
+    from blb_amd import reedsolomon as rs
+    text = open(HEADER).read()
+    codes = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define (BLBRS_\w+)\s+\(?(-?\d+)\)?", text)}
+    assert codes["BLBRS_ERR_INV_SHARD_NUM"] == rs.ErrInvShardNum.code
+    assert codes["BLBRS_ERR_MAX_SHARD_NUM"] == rs.ErrMaxShardNum.code
+    assert codes["BLBRS_ERR_TOO_FEW_SHARDS"] == rs.ErrTooFewShards.code
+    assert codes["BLBRS_ERR_SHARD_NO_DATA"] == rs.ErrShardNoData.code
+    assert codes["BLBRS_ERR_SHARD_SIZE"] == rs.ErrShardSize.code
+    assert codes["BLBRS_ERR_NO_DEVICE"] == rs.ErrNoDevice.code
+
+
+def test_new_errors_like_klauspost():
+    from blb_amd import reedsolomon as rs
+    with pytest.raises(rs.ErrInvShardNum):
+        rs.New(0, 3)
+    with pytest.raises(rs.ErrInvShardNum):
+        rs.New(6, 0)
+    with pytest.raises(rs.ErrInvShardNum):
+        rs.New(-1, 2)
+    with pytest.raises(rs.ErrMaxShardNum):
+        rs.New(250, 7)
+    enc = rs.New(250, 6)
+    assert enc.Shards == 256
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2), (6, 3), (8, 3), (10, 3), (10, 4), (12, 5), (20, 9)])
+def test_engine_matrix_matches_oracle(oracle_lib, k, m):
+    from blb_amd import reedsolomon as rs
+    assert np.array_equal(rs.New(k, m).matrix(), oracle_lib.build_matrix(k, m))
+
+
+def test_shard_checks_precede_device_use():
+    """klauspost's argument errors come before any GPU work (they hold with no GPU)."""
+    from blb_amd import reedsolomon as rs
+    enc = rs.New(3, 2)
+    S = 64
+    with pytest.raises(rs.ErrTooFewShards):
+        enc.Encode([np.zeros(S, np.uint8)] * 4)
+    with pytest.raises(rs.ErrShardNoData):
+        enc.Encode([np.zeros(0, np.uint8)] * 5)
+    with pytest.raises(rs.ErrShardSize):
+        enc.Encode([np.zeros(S, np.uint8)] * 4 + [np.zeros(S - 1, np.uint8)])
+    with pytest.raises(rs.ErrTooFewShards):
+        enc.Reconstruct([np.zeros(S, np.uint8), None, None, None, np.zeros(S, np.uint8)])
+    # all present: no work, no device needed (klauspost returns nil)
+    full = [np.zeros(S, np.uint8) for _ in range(5)]
+    enc.Reconstruct(full)
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from blb_amd import reedsolomon as rs
+    enc = rs.New(6, 3)
+    sh = [np.ones(128, np.uint8) for _ in range(9)]
+    with pytest.raises((rs.ErrNoDevice, rs.ErrHIP)):
+        enc.Encode(sh)
+
+
+def test_c_abi_null_arguments():
+    from blb_amd import _lib
+    lib = _lib.load()
+    assert lib.blbrs_new(3, 2, None) == -7
+    h = ctypes.c_void_p()
+    assert lib.blbrs_new(3, 2, ctypes.byref(h)) == 0
+    assert lib.blbrs_data_shards(h) == 3 and lib.blbrs_parity_shards(h) == 2
+    assert lib.blbrs_encode(h, None, None) == -7
+    small = (ctypes.c_uint8 * 4)()
+    assert lib.blbrs_matrix(h, small, 4) == -7
+    lib.blbrs_free(h)
+    assert lib.blbrs_strerror(-3).decode() == "too few shards given"
+    assert b"gfx950" in lib.blbrs_version()
