@@ -245,37 +245,29 @@ struct Stripes {
     bool aligned = false;
 };
 
-// Launch every pass of `plan` over `batch` stripes (split so B * tiles fits 32 bits).
+// Launch every pass of `plan` over `batch` stripes.
 int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mode mode,
              int32_t* mismatch, hipStream_t stream) {
     if (batch == 0 || S == 0) return BLBRS_OK;
-    const uint64_t tps = (S + tile_bytes() - 1) / tile_bytes();
-    const uint64_t max_b = std::max<uint64_t>(1, 0xFFFFFFFFull / tps);
-    for (size_t b0 = 0; b0 < batch; b0 += max_b) {
-        const size_t nb = std::min<uint64_t>(max_b, batch - b0);
-        for (const DevPass& ps : plan.passes) {
-            CodeArgs a{};
-            a.tables = ps.tables;
-            a.in_idx = ps.in_idx;
-            a.out_idx = ps.out_idx;
-            if (st.base) {
-                a.base = st.base + b0 * st.stripe_stride;
-            } else {
-                a.ptrs = st.ptrs + b0 * st.nshards;
-            }
-            a.shard_stride = st.shard_stride;
-            a.stripe_stride = st.stripe_stride;
-            a.nshards = st.nshards;
-            a.B = static_cast<uint32_t>(nb);
-            a.S = S;
-            a.tiles_per_stripe = static_cast<uint32_t>(tps);
-            a.k = ps.k_in;
-            a.rows = ps.rows;
-            a.aligned = st.aligned ? 1 : 0;
-            a.mismatch = mismatch ? mismatch + b0 : nullptr;
-            hipError_t e = launch_code(a, mode, stream);
-            if (e != hipSuccess) return hip_fail(e, "launch rs_code_kernel");
-        }
+    if (batch > 0x7FFFFFFFull) return fail(BLBRS_ERR_INVALID_ARG, "batch too large");
+    for (const DevPass& ps : plan.passes) {
+        CodeArgs a{};
+        a.tables = ps.tables;
+        a.in_idx = ps.in_idx;
+        a.out_idx = ps.out_idx;
+        a.base = st.base;
+        a.ptrs = st.ptrs;
+        a.shard_stride = st.shard_stride;
+        a.stripe_stride = st.stripe_stride;
+        a.nshards = st.nshards;
+        a.B = static_cast<uint32_t>(batch);
+        a.S = S;
+        a.k = ps.k_in;
+        a.rows = ps.rows;
+        a.aligned = st.aligned ? 1 : 0;
+        a.mismatch = mismatch;
+        hipError_t e = launch_code(a, mode, stream);
+        if (e != hipSuccess) return hip_fail(e, "launch rs_code_kernel");
     }
     return BLBRS_OK;
 }

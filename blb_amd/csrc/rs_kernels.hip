@@ -28,6 +28,8 @@
 //    construction because byte columns are independent.
 #include "rs_kernels.hpp"
 
+#include <algorithm>
+
 namespace blbrs {
 namespace {
 
@@ -84,6 +86,29 @@ __device__ __forceinline__ uint8_t* shard_ptr(const CodeArgs& a, uint32_t b, int
         return reinterpret_cast<uint8_t*>(as_const(a.ptrs)[static_cast<uint64_t>(b) * a.nshards + idx]);
 }
 
+using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+
+// 16-byte global load/store; NT bit 0 = nontemporal loads, bit 1 = nontemporal stores
+// (streamed data is touched exactly once).
+template <int NT>
+__device__ __forceinline__ V4 ld16(const uint8_t* p) {
+    if constexpr (NT & 1) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return V4{v.x, v.y, v.z, v.w};
+    } else {
+        return *reinterpret_cast<const V4*>(p);
+    }
+}
+template <int NT>
+__device__ __forceinline__ void st16(uint8_t* p, const V4& v) {
+    if constexpr (NT & 2) {
+        const u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+    } else {
+        *reinterpret_cast<V4*>(p) = v;
+    }
+}
+
 __device__ __forceinline__ V4 load_bytes(const uint8_t* p, uint32_t n) {
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     for (uint32_t j = 0; j < n; ++j) w[j >> 2] |= static_cast<uint32_t>(p[j]) << (8 * (j & 3));
@@ -99,7 +124,8 @@ __device__ __forceinline__ bool neq(const V4& a, const V4& b) {
     return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) != 0u;
 }
 
-// Byte-wise path for partial / unaligned tiles (runtime k, rows <= MR).
+// Partial / unaligned tiles (runtime k, rows <= MR): 16-byte vector accesses where a
+// chunk is whole and aligned, byte accesses for the shard's ragged end or unaligned shards.
 template <int MR, int MODE, int ADDR, int U>
 __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, uint64_t tile_off) {
     const int nr = a.rows;
@@ -107,10 +133,12 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
         const uint64_t off = tile_off + (static_cast<uint64_t>(u) * kThreads + threadIdx.x) * kBytesPerThread;
         if (off >= a.S) return;
         const uint32_t nb = static_cast<uint32_t>(a.S - off < 16 ? a.S - off : 16);
+        const bool vec = a.aligned && nb == 16;
         uint32_t acc[MR][4] = {};
         for (int c = 0; c < a.k; ++c) {
             uint32_t x[4];
-            unpack(load_bytes(shard_ptr<ADDR>(a, b, as_const(a.in_idx)[c]) + off, nb), x);
+            const uint8_t* p = shard_ptr<ADDR>(a, b, as_const(a.in_idx)[c]) + off;
+            unpack(vec ? ld16<0>(p) : load_bytes(p, nb), x);
             madd<MR, 4>(x, [&](int r) { return as_const(a.tables) + (static_cast<uint32_t>(r) * a.k + c) * 5; },
                         acc, nr);
         }
@@ -118,8 +146,12 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
         for (int r = 0; r < MR; ++r) {
             if (r >= nr) break;
             uint8_t* q = shard_ptr<ADDR>(a, b, as_const(a.out_idx)[r]) + off;
-            if constexpr (MODE == 0) store_bytes(q, pack(acc[r]), nb);
-            else if (neq(load_bytes(q, nb), pack(acc[r]))) atomicOr(&a.mismatch[b], 1);
+            if constexpr (MODE == 0) {
+                if (vec) st16<0>(q, pack(acc[r]));
+                else store_bytes(q, pack(acc[r]), nb);
+            } else if (neq(vec ? ld16<0>(q) : load_bytes(q, nb), pack(acc[r]))) {
+                atomicOr(&a.mismatch[b], 1);
+            }
         }
     }
 }
@@ -129,14 +161,18 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
 // MR: compile-time bound on output rows; a.rows <= MR honoured at runtime.
 // MODE 0 = store outputs, 1 = compare against existing outputs (Verify).
 // ADDR 0 = strided stripes, 1 = pointer table.  U = 16-byte chunks per lane per tile.
-template <int K, int MR, int MODE, int ADDR, int U>
+template <int K, int MR, int MODE, int ADDR, int U, int NT>
 __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
     constexpr uint32_t kTile = kTileBytes * U;
     const uint32_t total = a.B * a.tiles_per_stripe;
     const int nr = a.rows;
     const bool aligned = a.aligned != 0;
 
-    for (uint32_t t = blockIdx.x; t < total; t += gridDim.x) {
+    // Blocks are dealt round-robin over the 8 XCDs; with xcd_remap each XCD streams its own
+    // contiguous eighth of the (stripe, tile) space instead of every 8th tile.
+    uint32_t first = blockIdx.x;
+    if (a.xcd_remap) first = (first % 8u) * (gridDim.x / 8u) + first / 8u;
+    for (uint32_t t = first; t < total; t += gridDim.x) {
         const uint32_t b = t / a.tiles_per_stripe;
         const uint64_t tile_off = static_cast<uint64_t>(t - b * a.tiles_per_stripe) * kTile;
         if (!aligned || tile_off + kTile > a.S) {
@@ -161,7 +197,7 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
             for (int c = 0; c < K; ++c) {
                 const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
 #pragma unroll
-                for (int u = 0; u < U; ++u) x[c][u] = *reinterpret_cast<const V4*>(p + u * kStep);
+                for (int u = 0; u < U; ++u) x[c][u] = ld16<NT>(p + u * kStep);
             }
 #pragma unroll
             for (int c = 0; c < K; ++c) {
@@ -177,7 +213,7 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
                 const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
                 uint32_t xv[NV];
 #pragma unroll
-                for (int u = 0; u < U; ++u) unpack(*reinterpret_cast<const V4*>(p + u * kStep), xv + 4 * u);
+                for (int u = 0; u < U; ++u) unpack(ld16<NT>(p + u * kStep), xv + 4 * u);
                 madd<MR, NV>(xv, [&](int r) { return tables + (static_cast<uint32_t>(r) * k + c) * 5; }, acc, nr);
             }
         }
@@ -188,12 +224,12 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
             uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
             if constexpr (MODE == 0) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) *reinterpret_cast<V4*>(q + u * kStep) = pack(acc[r] + 4 * u);
+                for (int u = 0; u < U; ++u) st16<NT>(q + u * kStep, pack(acc[r] + 4 * u));
             } else {
                 bool bad = false;
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    bad |= neq(*reinterpret_cast<const V4*>(q + u * kStep), pack(acc[r] + 4 * u));
+                    bad |= neq(ld16<NT>(q + u * kStep), pack(acc[r] + 4 * u));
                 if (bad) atomicOr(&a.mismatch[b], 1);
             }
         }
@@ -208,88 +244,92 @@ using KernelFn = void (*)(CodeArgs);
 #define BLBRS_K_LIST(X) X(3) X(4) X(6) X(8) X(10) X(12)
 constexpr int kMaxTemplRows = 5;
 
-template <int K, int MODE, int ADDR, int U>
-KernelFn pick_rows(int rows) {
-    constexpr bool kGeneric = K == 0;
+// Launch policy, measured on MI355X (tools/tune_kernels.hip, profiles/r01/tune*.txt):
+//  * nontemporal loads and stores (every byte is touched once): +2-5 %;
+//  * U = 4 chunks per lane (16 KiB tiles) when the K*U + MR*U dwordx4 registers fit
+//    (K + MR <= 11), else U = 2 -- RS(10,4)/RS(12,5) at U = 4 hit 256 VGPRs and halve;
+//  * one tile per block in dispatch order (no persistent grid-stride), with each XCD given
+//    a contiguous eighth of the tiles: +10-16 % over a resident persistent grid.
+constexpr int kNT = 3;
+constexpr int pick_u(int K, int MR) { return (K > 0 && K + MR <= 11) ? 4 : 2; }
+
+template <int K, int MR, int MODE, int ADDR>
+constexpr KernelFn fn_of() { return rs_code_kernel<K, MR, MODE, ADDR, pick_u(K, MR), kNT>; }
+
+struct Choice {
+    KernelFn fn = nullptr;
+    int u = 0;
+    bool fixed = false;
+};
+
+template <int K, int MODE, int ADDR>
+Choice pick_rows(int rows) {
     switch (rows) {
-        case 1: return rs_code_kernel<K, 1, MODE, ADDR, U>;
-        case 2: return rs_code_kernel<K, 2, MODE, ADDR, U>;
-        case 3: return rs_code_kernel<K, 3, MODE, ADDR, U>;
-        case 4: return rs_code_kernel<K, 4, MODE, ADDR, U>;
-        case 5: return rs_code_kernel<K, 5, MODE, ADDR, U>;
-        case 6: return kGeneric ? rs_code_kernel<0, 6, MODE, ADDR, U> : nullptr;
-        case 7: return kGeneric ? rs_code_kernel<0, 7, MODE, ADDR, U> : nullptr;
-        case 8: return kGeneric ? rs_code_kernel<0, 8, MODE, ADDR, U> : nullptr;
-        default: return nullptr;
+        case 1: return {fn_of<K, 1, MODE, ADDR>(), pick_u(K, 1), K > 0};
+        case 2: return {fn_of<K, 2, MODE, ADDR>(), pick_u(K, 2), K > 0};
+        case 3: return {fn_of<K, 3, MODE, ADDR>(), pick_u(K, 3), K > 0};
+        case 4: return {fn_of<K, 4, MODE, ADDR>(), pick_u(K, 4), K > 0};
+        case 5: return {fn_of<K, 5, MODE, ADDR>(), pick_u(K, 5), K > 0};
+        case 6: return {fn_of<0, 6, MODE, ADDR>(), pick_u(0, 6), false};
+        case 7: return {fn_of<0, 7, MODE, ADDR>(), pick_u(0, 7), false};
+        case 8: return {fn_of<0, 8, MODE, ADDR>(), pick_u(0, 8), false};
+        default: return {};
     }
 }
 
-template <int MODE, int ADDR, int U>
-KernelFn pick_k(int k, int rows, bool* fixed) {
-    *fixed = true;
+template <int MODE, int ADDR>
+Choice pick_k(int k, int rows) {
     if (rows <= kMaxTemplRows) {
         switch (k) {
-#define BLBRS_CASE(KK) case KK: return pick_rows<KK, MODE, ADDR, U>(rows);
+#define BLBRS_CASE(KK) case KK: return pick_rows<KK, MODE, ADDR>(rows);
             BLBRS_K_LIST(BLBRS_CASE)
 #undef BLBRS_CASE
             default: break;
         }
     }
-    *fixed = false;
-    return pick_rows<0, MODE, ADDR, U>(rows);
+    return pick_rows<0, MODE, ADDR>(rows);
 }
 
-constexpr int kU = 2;  // chunks per lane per tile (8 KiB column tiles)
-
-KernelFn pick(int k, int rows, Mode mode, bool strided, bool* fixed) {
-    if (mode == Mode::kStore)
-        return strided ? pick_k<0, 0, kU>(k, rows, fixed) : pick_k<0, 1, kU>(k, rows, fixed);
-    return strided ? pick_k<1, 0, kU>(k, rows, fixed) : pick_k<1, 1, kU>(k, rows, fixed);
-}
-
-int blocks_per_cu(KernelFn fn) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(fn), kThreads, 0) !=
-            hipSuccess || n <= 0)
-        n = 4;
-    return n;
-}
-
-int cu_count() {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-        n = 256;
-    return n;
+Choice pick(int k, int rows, Mode mode, bool strided) {
+    if (mode == Mode::kStore) return strided ? pick_k<0, 0>(k, rows) : pick_k<0, 1>(k, rows);
+    return strided ? pick_k<1, 0>(k, rows) : pick_k<1, 1>(k, rows);
 }
 
 }  // namespace
 
-uint32_t tile_bytes() { return static_cast<uint32_t>(kTileBytes) * kU; }
-
 hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream) {
     if (args.rows < 1 || args.rows > kMaxRows || args.k < 1) return hipErrorInvalidValue;
     if (args.B == 0 || args.S == 0) return hipSuccess;
-    bool fixed = false;
-    KernelFn fn = pick(args.k, args.rows, mode, args.base != nullptr, &fixed);
-    if (!fn) return hipErrorInvalidValue;
-    // Resident-grid sizing: blocks grid-stride over (stripe, tile); CUs x resident blocks
-    // keeps all 256 CUs streaming with no tail wave of late blocks.
-    static thread_local KernelFn last_fn = nullptr;
-    static thread_local int last_bpc = 0, last_cus = 0;
-    if (fn != last_fn) { last_bpc = blocks_per_cu(fn); last_cus = cu_count(); last_fn = fn; }
-    const uint64_t total = static_cast<uint64_t>(args.B) * args.tiles_per_stripe;
-    uint64_t grid = static_cast<uint64_t>(last_cus) * static_cast<uint64_t>(last_bpc);
-    if (grid > total) grid = total;
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream, args);
-    return hipGetLastError();
+    const Choice ch = pick(args.k, args.rows, mode, args.base != nullptr);
+    if (!ch.fn) return hipErrorInvalidValue;
+    const uint64_t tile = static_cast<uint64_t>(kTileBytes) * ch.u;
+    const uint64_t tps = (args.S + tile - 1) / tile;
+    // Tiles are numbered with 32-bit ints: split huge batches.
+    const uint64_t max_b = std::max<uint64_t>(1, 0x7FFFFFFFull / tps);
+    for (uint64_t b0 = 0; b0 < args.B; b0 += max_b) {
+        CodeArgs a = args;
+        a.B = static_cast<uint32_t>(std::min<uint64_t>(max_b, args.B - b0));
+        if (a.base) a.base += b0 * a.stripe_stride;
+        else a.ptrs += b0 * a.nshards;
+        if (a.mismatch) a.mismatch += b0;
+        a.tiles_per_stripe = static_cast<uint32_t>(tps);
+        const uint64_t total = static_cast<uint64_t>(a.B) * tps;
+        uint64_t grid = total;
+        a.xcd_remap = 0;
+        if (total >= 64) {  // one tile per block; a multiple of 8 blocks for the XCD remap
+            grid = total & ~uint64_t{7};
+            a.xcd_remap = 1;
+        }
+        hipLaunchKernelGGL(ch.fn, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 const char* kernel_name(int k, int rows, Mode mode) {
-    bool fixed = false;
-    pick(k, rows, mode, true, &fixed);
-    return fixed ? "rs_code_kernel<K,MR,MODE,ADDR,U>" : "rs_code_kernel<0,MR,MODE,ADDR,U>";
+    const Choice ch = pick(k, rows, mode, true);
+    return ch.fixed ? "rs_code_kernel<K,MR,MODE,ADDR,U,NT>" : "rs_code_kernel<0,MR,MODE,ADDR,U,NT>";
 }
 
 }  // namespace blbrs

@@ -20,11 +20,12 @@ struct CodeArgs {
     uint32_t nshards;         //   k+m entries per stripe
     uint32_t B;               // stripes in the batch
     uint64_t S;               // shard length in bytes
-    uint32_t tiles_per_stripe;
+    uint32_t tiles_per_stripe;  // set by launch_code()
     int32_t k;                // inputs per stripe
     int32_t rows;             // outputs per stripe (<= kMaxRows)
     int32_t aligned;          // every shard address 16-byte aligned (vector path allowed)
     int32_t* mismatch;        // verify: [B] flags (device)
+    int32_t xcd_remap;        // set by launch_code(): block b starts at tile (b%8)*(grid/8) + b/8
 };
 
 constexpr int kThreads = 256;
@@ -34,13 +35,12 @@ constexpr int kMaxRows = 8;                               // outputs per pass
 
 enum class Mode : int { kStore = 0, kVerify = 1 };
 
-// Launches one pass on `stream`; returns hipSuccess or the launch error.
+// Launches one pass over args.B stripes on `stream` (grid, tiles and XCD mapping chosen
+// here); returns hipSuccess or the launch error.
 hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream);
 
 // Name of the kernel instantiation launch_code() would pick (for profiling/tests).
 const char* kernel_name(int k, int rows, Mode mode);
 
-// Column bytes one block-iteration covers; CodeArgs::tiles_per_stripe = ceil(S / this).
-uint32_t tile_bytes();
 
 }  // namespace blbrs

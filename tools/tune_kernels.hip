@@ -1,0 +1,155 @@
+// tune_kernels.hip -- standalone MI355X tuning harness for the RS coding kernel.
+// Measures, on the BASELINE workload (RS(6,3), B stripes of 8 MiB shards, strided):
+//   * the access-pattern ceiling: read R shards / write W shards with trivial XOR compute;
+//   * rs_code_kernel variants: chunks per lane U, nontemporal policy NT, grid size.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/tune_kernels.hip -o tools/_build/tune
+#include "../blb_amd/csrc/rs_kernels.hip"
+#include "../blb_amd/csrc/gf256.hpp"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace blbrs;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1); } } while (0)
+
+// Pattern kernel: each lane reads U 16B chunks from each of R shards, XORs them and writes
+// the XOR to W shards.
+template <int R, int W, int U, int NT, int XCD = 0>
+__global__ __launch_bounds__(256) void pattern_kernel(uint8_t* base, uint64_t shard_stride, uint64_t stripe_stride,
+                                                      uint32_t B, uint32_t tps, uint32_t* sink) {
+    constexpr uint32_t kStep = 256 * 16;
+    const uint32_t total = B * tps;
+    uint32_t keep = 0;
+    uint32_t bid = blockIdx.x;
+    if (XCD) bid = (bid % 8) * (gridDim.x / 8) + bid / 8;  // XCD x owns a contiguous block range
+    for (uint32_t t = bid; t < total; t += gridDim.x) {
+        const uint32_t b = t / tps;
+        const uint64_t off = static_cast<uint64_t>(t - b * tps) * kStep * U + threadIdx.x * 16;
+        uint8_t* s = base + b * stripe_stride + off;
+        V4 x[R][U];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[r][u] = ld16<NT>(s + r * shard_stride + u * kStep);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            V4 a{0, 0, 0, 0};
+#pragma unroll
+            for (int r = 0; r < R; ++r) { a.x ^= x[r][u].x; a.y ^= x[r][u].y; a.z ^= x[r][u].z; a.w ^= x[r][u].w; }
+            if constexpr (W == 0) keep ^= a.x ^ a.y ^ a.z ^ a.w;
+#pragma unroll
+            for (int w = 0; w < W; ++w) st16<NT>(s + (R + w) * shard_stride + u * kStep, a);
+        }
+    }
+    if (W == 0 && keep == 0x9E3779B9u) sink[0] = keep;
+}
+
+struct Timer {
+    hipEvent_t a, b;
+    Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
+};
+
+template <typename F>
+double time_ms(F launch, int reps = 10) {
+    static Timer t;
+    launch(); launch();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(t.a));
+    for (int i = 0; i < reps; ++i) launch();
+    CK(hipEventRecord(t.b));
+    CK(hipEventSynchronize(t.b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, t.a, t.b));
+    return ms / reps;
+}
+
+static uint8_t* g_base;
+static uint32_t* g_sink;
+static const uint64_t S = 8ull << 20;
+static uint32_t B = 1024;
+
+template <int R, int W, int U, int NT, int XCD = 0>
+void run_pattern(int grid) {
+    const uint64_t ss = S, bs = 9 * S;
+    const uint32_t tps = static_cast<uint32_t>(S / (4096 * U));
+    double ms = time_ms([&] { hipLaunchKernelGGL((pattern_kernel<R, W, U, NT, XCD>), dim3(grid), dim3(256), 0, 0,
+                                                 g_base, ss, bs, B, tps, g_sink); });
+    const double bytes = double(B) * (R + W) * S;
+    printf("pattern XCD=%d R=%d W=%d U=%d NT=%d grid=%6d : %8.3f ms  %7.1f GB/s\n", XCD, R, W, U, NT, grid, ms, bytes / ms / 1e6);
+}
+
+template <int U, int NT, int K = 6, int MR = 3, int MODE = 0>
+void run_rs(CodeArgs a, int grid, const char* tag, int remap = 0) {
+    a.xcd_remap = remap;
+    a.tiles_per_stripe = static_cast<uint32_t>(S / (kTileBytes * U));
+    auto fn = rs_code_kernel<K, MR, MODE, 0, U, NT>;
+    int bpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(fn), 256, 0));
+    if (grid <= 0) grid = 256 * bpc * (-grid == 0 ? 1 : -grid);
+    if (grid == 1) grid = static_cast<int>(a.B * a.tiles_per_stripe);
+    double ms = time_ms([&] { hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, 0, a); });
+    const int kk = K ? K : a.k;
+    const double bytes = double(a.B) * (kk + MR) * S;
+    printf("K=%2d MR=%d MODE=%d %-6s remap=%d U=%d NT=%d bpc=%d grid=%7d : %8.3f ms  %7.1f GB/s  %7.1f GiB/s data\n",
+           kk, MR, MODE, tag, remap, U, NT, bpc, grid, ms, bytes / ms / 1e6,
+           double(a.B) * kk * S / (ms * 1e-3) / double(1u << 30));
+}
+
+int main(int argc, char** argv) {
+    if (argc > 1) B = static_cast<uint32_t>(atoi(argv[1]));
+    const size_t total = size_t(B) * 9 * S;
+    CK(hipMalloc(&g_base, total));
+    CK(hipMalloc(&g_sink, 64));
+    CK(hipMemset(g_base, 0x5B, total));
+    // tables for RS(6,3)
+    Mat mat;
+    build_matrix(6, 3, mat);
+    std::vector<uint32_t> tab(17 * 8 * 5, 0x03020100u);
+    int32_t idx[32];
+    for (int i = 0; i < 32; ++i) idx[i] = i;
+    uint32_t* d_tab; int32_t* d_idx;
+    CK(hipMalloc(&d_tab, tab.size() * 4));
+    CK(hipMalloc(&d_idx, sizeof(idx)));
+    CK(hipMemcpy(d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_idx, idx, sizeof(idx), hipMemcpyHostToDevice));
+    int32_t* d_flags;
+    CK(hipMalloc(&d_flags, 1 << 20));
+    CK(hipMemset(d_flags, 0, 1 << 20));
+    CodeArgs a{};
+    a.tables = d_tab; a.in_idx = d_idx; a.out_idx = d_idx + 6; a.base = g_base;
+    a.shard_stride = S; a.stripe_stride = 9 * S; a.B = B; a.S = S; a.k = 6; a.rows = 3; a.aligned = 1;
+    a.mismatch = d_flags;
+    // same 72 GiB buffer re-viewed for the other shapes
+    auto shape = [&](int k, int rows) {
+        CodeArgs c = a;
+        c.k = k; c.rows = rows; c.out_idx = d_idx + k;
+        c.stripe_stride = uint64_t(k + rows) * S;
+        c.B = static_cast<uint32_t>(total / c.stripe_stride);
+        return c;
+    };
+
+    printf("# B=%u stripes x 9 shards x 8 MiB = %.1f GiB\n", B, total / double(1ull << 30));
+    for (int rep = 0; rep < 2; ++rep) {
+        printf("# rep %d\n", rep);
+        run_rs<4, 3>(a, 1, "all", 1);
+        run_rs<2, 3>(a, 1, "all", 1);
+        run_rs<4, 3, 6, 1>(shape(6, 1), 1, "dec1", 1);
+        run_rs<2, 3, 6, 1>(shape(6, 1), 1, "dec1", 1);
+        run_rs<4, 1, 6, 3, 1>(a, 1, "verify", 1);
+        run_rs<2, 1, 6, 3, 1>(a, 1, "verify", 1);
+        run_rs<4, 3, 10, 4>(shape(10, 4), 1, "rs104", 1);
+        run_rs<2, 3, 10, 4>(shape(10, 4), 1, "rs104", 1);
+        run_rs<4, 3, 10, 2>(shape(10, 2), 1, "dec2", 1);
+        run_rs<2, 3, 10, 2>(shape(10, 2), 1, "dec2", 1);
+        run_rs<4, 3, 12, 5>(shape(12, 5), 1, "rs125", 1);
+        run_rs<2, 3, 12, 5>(shape(12, 5), 1, "rs125", 1);
+        run_rs<4, 3, 8, 3>(shape(8, 3), 1, "rs83", 1);
+        run_rs<2, 3, 8, 3>(shape(8, 3), 1, "rs83", 1);
+        run_rs<4, 3, 0, 3>(shape(17, 3), 1, "gen17", 1);
+        run_rs<2, 3, 0, 3>(shape(17, 3), 1, "gen17", 1);
+        run_rs<1, 3, 0, 3>(shape(17, 3), 1, "gen17", 1);
+    }
+    return 0;
+}
