@@ -25,6 +25,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from blb_amd import multigpu  # noqa: E402
 from blb_amd import reedsolomon as rs  # noqa: E402
 
 GIB = float(1 << 30)
@@ -41,7 +42,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--k", type=int, default=6)
     p.add_argument("--m", type=int, default=3)
-    p.add_argument("--batch", type=int, default=1024, help="stripes per GPU")
+    p.add_argument("--batch", type=int, default=1024, help="stripes per GPU (weak scaling)")
+    p.add_argument("--total-batch", type=int, default=0,
+                   help="if set: stripes for the whole job, split over ranks (strong scaling, "
+                        "e.g. BASELINE config 4: --k 10 --m 4 --total-batch 4096)")
     p.add_argument("--shard", type=int, default=TRACT)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-extra", action="store_true", help="skip decode / PCIe side measurements")
@@ -99,9 +103,8 @@ def cpu_baseline(k, m, seconds):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    r = multigpu.env_rank()
+    world, rank, local = r.world, r.rank, r.local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -109,7 +112,11 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    k, m, B, S = a.k, a.m, a.batch, a.shard
+    k, m, S = a.k, a.m, a.shard
+    if a.total_batch:
+        _, B = multigpu.stripe_range(a.total_batch, world, rank)
+    else:
+        B = a.batch
     enc = rs.New(k, m)
     stripes = torch.empty((B, k + m, S), dtype=torch.uint8, device=dev)
     g = torch.Generator(device=dev)
@@ -135,17 +142,13 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt_local = time.perf_counter() - t0
+    dt = multigpu.max_over_ranks(dt_local, dev)
+    value = multigpu.aggregate_gibps(float(B * k * S * a.steps), dt_local, dev)
 
     launch_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
     algo_bytes = B * (k + m) * S
     achieved_gbs = algo_bytes / (launch_ms * 1e-3) / 1e9
-    data_bytes_total = world * B * k * S * a.steps
-    value = data_bytes_total / GIB / dt
 
     extra = {}
     cpu = None
@@ -192,11 +195,13 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.total_batch else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded uniform random bytes, device-resident)",
-            "config": {"workload": f"RS({k},{m}) encode, batch={B} stripes of {S // (1 << 20)} MiB tracts per GPU",
+            "config": {"workload": (f"RS({k},{m}) encode, batch={a.total_batch} stripes of {S // (1 << 20)} MiB "
+                                    f"tracts split over {world} GPU(s)") if a.total_batch else
+                                   f"RS({k},{m}) encode, batch={B} stripes of {S // (1 << 20)} MiB tracts per GPU",
                        "k": k, "m": m, "batch_per_gpu": B, "shard_bytes": S,
                        "parallelism": f"stripe-batch split x{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,

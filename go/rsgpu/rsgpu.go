@@ -1,0 +1,199 @@
+// Package rsgpu is the cgo binding of libblbrs.so (include/blb_rs.h): a drop-in
+// reedsolomon.Encoder for blb whose Encode / Verify / Reconstruct / ReconstructData run on
+// MI355X HIP kernels.
+//
+// It replaces github.com/klauspost/reedsolomon (@925cb01d6510, blb go.mod:20) at blb's call
+// sites without changing their call surface:
+//
+//	internal/tractserver/store.go:1022   enc, e := reedsolomon.New(N, M)  ->  rsgpu.New(N, M)
+//	client/blb/reconstruct.go:166        enc, e := reedsolomon.New(n, m)  ->  rsgpu.New(n, m)
+//
+// The returned value satisfies reedsolomon.Encoder (store.go:1042,1132 take that type).
+// Split / Join / Update are not on blb's path; they are delegated to klauspost's CPU encoder.
+//
+// Source only in this repository: this image has no Go toolchain (SURVEY.md §0.4).  Build
+// where Go >= 1.21 (runtime.Pinner) and the library exist:
+//
+//	CGO_CFLAGS=-I<repo>/include CGO_LDFLAGS="-L<repo>/blb_amd -lblbrs -Wl,-rpath,<repo>/blb_amd" go build
+package rsgpu
+
+/*
+#cgo LDFLAGS: -lblbrs
+#include <stdlib.h>
+#include <stdint.h>
+#include "blb_rs.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"io"
+	"runtime"
+	"unsafe"
+
+	"github.com/klauspost/reedsolomon"
+)
+
+// Map the C ABI's codes (blb_rs.h) back onto klauspost's exported error values, so
+// callers comparing against reedsolomon.ErrTooFewShards etc. keep working.
+func mapErr(rc C.int) error {
+	switch rc {
+	case C.BLBRS_OK:
+		return nil
+	case C.BLBRS_ERR_INV_SHARD_NUM:
+		return reedsolomon.ErrInvShardNum
+	case C.BLBRS_ERR_MAX_SHARD_NUM:
+		return reedsolomon.ErrMaxShardNum
+	case C.BLBRS_ERR_TOO_FEW_SHARDS:
+		return reedsolomon.ErrTooFewShards
+	case C.BLBRS_ERR_SHARD_NO_DATA:
+		return reedsolomon.ErrShardNoData
+	case C.BLBRS_ERR_SHARD_SIZE:
+		return reedsolomon.ErrShardSize
+	default:
+		return errors.New("rsgpu: " + C.GoString(C.blbrs_last_error()))
+	}
+}
+
+type encoder struct {
+	h   *C.blbrs_encoder
+	k   int
+	m   int
+	cpu reedsolomon.Encoder // Split / Join / Update only
+}
+
+// New is reedsolomon.New(dataShards, parityShards) backed by the GPU engine.
+func New(dataShards, parityShards int) (reedsolomon.Encoder, error) {
+	var h *C.blbrs_encoder
+	if rc := C.blbrs_new(C.int(dataShards), C.int(parityShards), &h); rc != C.BLBRS_OK {
+		return nil, mapErr(rc)
+	}
+	cpu, err := reedsolomon.New(dataShards, parityShards)
+	if err != nil {
+		C.blbrs_free(h)
+		return nil, err
+	}
+	e := &encoder{h: h, k: dataShards, m: parityShards, cpu: cpu}
+	runtime.SetFinalizer(e, func(e *encoder) { C.blbrs_free(e.h) })
+	return e, nil
+}
+
+// marshal builds C arrays of shard pointers and lengths.  cgo forbids storing Go pointers
+// in C memory unless they are pinned, so every non-empty shard is pinned for the call;
+// the C side does not retain any pointer after returning.  A missing shard that has
+// capacity (klauspost reslices shards[i][0:size] when cap >= size; client/blb/
+// reconstruct.go:172 relies on it) passes its backing array as the output buffer.
+type marshalled struct {
+	ptrs   *unsafe.Pointer
+	lens   *C.size_t
+	pinner runtime.Pinner
+}
+
+func marshal(shards [][]byte, size int) *marshalled {
+	n := len(shards)
+	mm := &marshalled{
+		ptrs: (*unsafe.Pointer)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0))))),
+		lens: (*C.size_t)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.size_t(0))))),
+	}
+	ptrs := unsafe.Slice(mm.ptrs, n)
+	lens := unsafe.Slice(mm.lens, n)
+	for i, s := range shards {
+		lens[i] = C.size_t(len(s))
+		ptrs[i] = nil
+		if cap(s) > 0 && (len(s) > 0 || cap(s) >= size) {
+			p := &s[:1][0]
+			mm.pinner.Pin(p)
+			ptrs[i] = unsafe.Pointer(p)
+		}
+	}
+	return mm
+}
+
+func (mm *marshalled) free() {
+	mm.pinner.Unpin()
+	C.free(unsafe.Pointer(mm.ptrs))
+	C.free(unsafe.Pointer(mm.lens))
+}
+
+func shardSize(shards [][]byte) int {
+	for _, s := range shards {
+		if len(s) != 0 {
+			return len(s)
+		}
+	}
+	return 0
+}
+
+func (e *encoder) Encode(shards [][]byte) error {
+	if len(shards) != e.k+e.m {
+		return reedsolomon.ErrTooFewShards
+	}
+	mm := marshal(shards, shardSize(shards))
+	defer mm.free()
+	return mapErr(C.blbrs_encode(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens))
+}
+
+func (e *encoder) Verify(shards [][]byte) (bool, error) {
+	if len(shards) != e.k+e.m {
+		return false, reedsolomon.ErrTooFewShards
+	}
+	mm := marshal(shards, shardSize(shards))
+	defer mm.free()
+	var ok C.int
+	if rc := C.blbrs_verify(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens, &ok); rc != C.BLBRS_OK {
+		return false, mapErr(rc)
+	}
+	return ok != 0, nil
+}
+
+func (e *encoder) reconstruct(shards [][]byte, dataOnly bool) error {
+	if len(shards) != e.k+e.m {
+		return reedsolomon.ErrTooFewShards
+	}
+	size := shardSize(shards)
+	present := 0
+	for _, s := range shards {
+		if len(s) != 0 {
+			present++
+		}
+	}
+	// klauspost allocates a missing output whose cap is too small -- only once the
+	// argument checks have passed; do the same so the C side always has a buffer (data
+	// slots always, parity slots unless dataOnly).  Error cases fall through to C.
+	if size > 0 && present >= e.k && present < e.k+e.m {
+		for i := range shards {
+			if len(shards[i]) == 0 && cap(shards[i]) < size && (i < e.k || !dataOnly) {
+				shards[i] = make([]byte, 0, size)
+			}
+		}
+	}
+	mm := marshal(shards, size)
+	defer mm.free()
+	var rc C.int
+	if dataOnly {
+		rc = C.blbrs_reconstruct_data(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens)
+	} else {
+		rc = C.blbrs_reconstruct(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens)
+	}
+	if rc != C.BLBRS_OK {
+		return mapErr(rc)
+	}
+	lens := unsafe.Slice(mm.lens, len(shards))
+	for i := range shards {
+		if len(shards[i]) == 0 && lens[i] != 0 {
+			shards[i] = shards[i][0:size] // output landed in the caller's backing array
+		}
+	}
+	return nil
+}
+
+func (e *encoder) Reconstruct(shards [][]byte) error     { return e.reconstruct(shards, false) }
+func (e *encoder) ReconstructData(shards [][]byte) error { return e.reconstruct(shards, true) }
+
+func (e *encoder) Update(shards [][]byte, newDatashards [][]byte) error {
+	return e.cpu.Update(shards, newDatashards)
+}
+func (e *encoder) Split(data []byte) ([][]byte, error) { return e.cpu.Split(data) }
+func (e *encoder) Join(dst io.Writer, shards [][]byte, outSize int) error {
+	return e.cpu.Join(dst, shards, outSize)
+}

@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 using namespace blbrs;
@@ -98,7 +99,8 @@ void run_rs(CodeArgs a, int grid, const char* tag, int remap = 0) {
 }
 
 int main(int argc, char** argv) {
-    if (argc > 1) B = static_cast<uint32_t>(atoi(argv[1]));
+    const bool pmc = argc > 1 && std::string(argv[1]) == "pmc";
+    if (argc > 1 && !pmc) B = static_cast<uint32_t>(atoi(argv[1]));
     const size_t total = size_t(B) * 9 * S;
     CK(hipMalloc(&g_base, total));
     CK(hipMalloc(&g_sink, 64));
@@ -131,6 +133,25 @@ int main(int argc, char** argv) {
     };
 
     printf("# B=%u stripes x 9 shards x 8 MiB = %.1f GiB\n", B, total / double(1ull << 30));
+    if (pmc) {
+        // Counter calibration (one launch each, run under rocprofv3 --pmc):
+        //   pattern R=9 W=0: reads exactly B*9*S bytes, writes nothing;
+        //   pattern R=1 W=1: reads B*S, writes B*S (same nt 16-B/lane access as the kernel);
+        //   rs_code_kernel<6,3,0,0,4,3>: the production RS(6,3) encode.
+        const uint32_t all4 = static_cast<uint32_t>(B * (S / 16384));
+        hipLaunchKernelGGL((pattern_kernel<9, 0, 4, 3, 1>), dim3(all4 & ~7u), dim3(256), 0, 0, g_base, S, 9 * S, B,
+                           static_cast<uint32_t>(S / 16384), g_sink);
+        hipLaunchKernelGGL((pattern_kernel<1, 1, 4, 3, 1>), dim3(all4 & ~7u), dim3(256), 0, 0, g_base, S, 9 * S, B,
+                           static_cast<uint32_t>(S / 16384), g_sink);
+        CodeArgs c = a;
+        c.tiles_per_stripe = static_cast<uint32_t>(S / 16384);
+        c.xcd_remap = 1;
+        hipLaunchKernelGGL((rs_code_kernel<6, 3, 0, 0, 4, 3>), dim3(all4 & ~7u), dim3(256), 0, 0, c);
+        CK(hipDeviceSynchronize());
+        printf("pmc launches done: read_bytes=%.0f copy_bytes=%.0f+%.0f rs63_bytes=%.0f+%.0f\n", double(B) * 9 * S,
+               double(B) * S, double(B) * S, double(B) * 6 * S, double(B) * 3 * S);
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         printf("# rep %d\n", rep);
         run_rs<4, 3>(a, 1, "all", 1);
