@@ -7,25 +7,27 @@
 //
 // Design (MI355X-first, byte-wise integer work -> HBM-bound, no MFMA):
 //  * A block of 256 threads owns a column tile of one stripe; each lane moves U 16-byte
-//    dwordx4 chunks per shard, so every wave reads k*U coalesced 1 KiB segments and
-//    writes rows*U.  Blocks grid-stride over (stripe, tile), the grid sized to the
-//    resident-block count, so the batch streams through HBM once with nothing re-read.
+//    dwordx4 chunks per shard (U = 4 or 2), so every wave reads k*U coalesced 1 KiB
+//    segments and writes rows*U.  One tile per block in dispatch order, and each XCD gets a
+//    contiguous eighth of the (stripe, tile) space; loads and stores are nontemporal since
+//    every byte is touched exactly once.  Nothing is re-read: PMC traffic = algorithmic
+//    bytes (profiles/pmc_r01_rs63_encode.json).
 //  * GF multiply by a constant uses register lookup tables and v_perm_b32:
 //    byte x = g0 | g1<<3 | g2<<6 (3+3+2 bits) and c*x = T0[g0]^T1[g1]^T2[g2]; each table
 //    has <= 8 one-byte entries, so one v_perm_b32 byte-select over two dwords looks up 4
 //    bytes at once.  Cost: 5 VALU per input dword for the bit groups (shared by every
-//    output row) + 3 perms + 3 xors per (coefficient, dword).  RS(6,3) needs ~23 VALU per
-//    4 input bytes, about a third of the HBM time at full VALU rate: the kernel stays
-//    memory-bound.  LDS log/antilog lookups would need k*m ds_read_u8 per byte with random
-//    bank conflicts and cap well below the roofline (SURVEY.md §7 "Hard parts").
-//  * Coefficient tables (5 dwords per coefficient) are wave-uniform and re-read with
-//    scalar loads each tile (scalar-cache hits) instead of being pinned for the whole
-//    launch, which would overflow the SGPR file and spill through v_writelane/readlane.
+//    output row) + 3 perms + 1.5 v_bitop3 XOR3 per (coefficient, dword).  RS(6,3) needs
+//    ~19 VALU per 4 input bytes, well under the HBM time at full VALU rate.  LDS
+//    log/antilog lookups would need k*m ds_read_u8 per byte with random bank conflicts and
+//    cap well below the roofline (SURVEY.md §7 "Hard parts").
+//  * Coefficient tables (5 dwords per coefficient) are wave-uniform, read through the
+//    constant address space with scalar loads each tile (scalar-cache hits) instead of
+//    being pinned for the whole launch, which would overflow the SGPR file.
 //  * Every output byte is written, never accumulated into: callers hand in un-zeroed
 //    pooled buffers (pkg/rpc/pool.go:28-43).
-//  * A tile that is not entirely inside the shard (length not a multiple of the tile) or
-//    whose shards are not 16-byte aligned takes a byte-wise path; results are identical by
-//    construction because byte columns are independent.
+//  * A tile that is not entirely inside the shard, or whose shards are not 16-byte
+//    aligned, takes a per-lane path (vector where a 16-byte chunk is whole, bytes for the
+//    ragged end); results are identical because byte columns are independent.
 #include "rs_kernels.hpp"
 
 #include <algorithm>
@@ -44,32 +46,77 @@ __device__ __forceinline__ cu32 as_const(const uint32_t* p) { return (cu32)(uint
 __device__ __forceinline__ ci32 as_const(const int32_t* p) { return (ci32)(uintptr_t)p; }
 __device__ __forceinline__ cu64 as_const(const uint64_t* p) { return (cu64)(uintptr_t)p; }
 
-template <typename TP>
-__device__ __forceinline__ uint32_t gmul(TP t, uint32_t g0, uint32_t g1, uint32_t g2) {
-    return __builtin_amdgcn_perm(t[1], t[0], g0) ^ __builtin_amdgcn_perm(t[3], t[2], g1) ^
-           __builtin_amdgcn_perm(0u, t[4], g2);
+
+// 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96 = a ^ b ^ c); hipcc
+// does not form it from a ^ b ^ c by itself.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// acc[r] ^= coef(r, c) * x over NV input dwords of ONE input shard c.  Bit groups are
-// split once per dword and shared by every row; each row's 5 table words are fetched once
-// and applied to all NV dwords (amortises the SGPR->VGPR moves v_perm needs for its
-// second table operand under gfx9's one-SGPR constant-bus limit).
-template <int MR, int NV, typename Tab>
-__device__ __forceinline__ void madd(const uint32_t (&x)[NV], Tab tab, uint32_t (&acc)[MR][NV], int nr) {
+// Bit groups of NV input dwords: g0 = x[2:0], g1 = x[5:3], g2 = x[7:6] of every byte
+// (5 VALU per dword, shared by every output row).
+template <int NV>
+struct Groups {
     uint32_t g0[NV], g1[NV], g2[NV];
+    __device__ __forceinline__ explicit Groups(const uint32_t (&x)[NV]) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        g0[v] = x[v] & 0x07070707u;
-        g1[v] = (x[v] >> 3) & 0x07070707u;
-        g2[v] = (x[v] >> 6) & 0x03030303u;
+        for (int v = 0; v < NV; ++v) {
+            g0[v] = x[v] & 0x07070707u;
+            g1[v] = (x[v] >> 3) & 0x07070707u;
+            g2[v] = (x[v] >> 6) & 0x03030303u;
+        }
     }
+};
+
+template <typename TP>
+__device__ __forceinline__ void load_tab(TP tp, uint32_t (&t)[5]) {
+#pragma unroll
+    for (int w = 0; w < 5; ++w) t[w] = tp[w];
+}
+
+// acc[r] ^= coef(r, c) * x over NV input dwords of ONE input shard c: 3 v_perm + 2 xor3
+// ... per (row, dword).  Each row's 5 table words are fetched once and applied to all NV
+// dwords (amortises the SGPR->VGPR moves v_perm needs for its second table operand under
+// gfx9's one-SGPR constant-bus limit).
+template <int MR, int NV, typename Tab>
+__device__ __forceinline__ void madd(const Groups<NV>& g, Tab tab, uint32_t (&acc)[MR][NV], int nr) {
 #pragma unroll
     for (int r = 0; r < MR; ++r) {
         if (r < nr) {
-            const auto tp = tab(r);
-            const uint32_t t[5] = {tp[0], tp[1], tp[2], tp[3], tp[4]};
+            uint32_t t[5];
+            load_tab(tab(r), t);
 #pragma unroll
-            for (int v = 0; v < NV; ++v) acc[r][v] ^= gmul(t, g0[v], g1[v], g2[v]);
+            for (int v = 0; v < NV; ++v) {
+                const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], g.g0[v]);
+                const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], g.g1[v]);
+                const uint32_t p2 = __builtin_amdgcn_perm(0u, t[4], g.g2[v]);
+                acc[r][v] = xor3(xor3(acc[r][v], p0, p1), p2, 0u);
+            }
+        }
+    }
+}
+
+// Two input shards at once: 6 perm terms + acc folded by 3 xor3 (1.5 VALU per coefficient
+// and dword instead of 3 plain XORs).
+template <int MR, int NV, typename TabA, typename TabB>
+__device__ __forceinline__ void madd2(const Groups<NV>& ga, TabA taba, const Groups<NV>& gb, TabB tabb,
+                                      uint32_t (&acc)[MR][NV], int nr) {
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+        if (r < nr) {
+            uint32_t a[5], b[5];
+            load_tab(taba(r), a);
+            load_tab(tabb(r), b);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const uint32_t a0 = __builtin_amdgcn_perm(a[1], a[0], ga.g0[v]);
+                const uint32_t a1 = __builtin_amdgcn_perm(a[3], a[2], ga.g1[v]);
+                const uint32_t a2 = __builtin_amdgcn_perm(0u, a[4], ga.g2[v]);
+                const uint32_t b0 = __builtin_amdgcn_perm(b[1], b[0], gb.g0[v]);
+                const uint32_t b1 = __builtin_amdgcn_perm(b[3], b[2], gb.g1[v]);
+                const uint32_t b2 = __builtin_amdgcn_perm(0u, b[4], gb.g2[v]);
+                acc[r][v] = xor3(xor3(xor3(acc[r][v], a0, a1), a2, b0), b1, b2);
+            }
         }
     }
 }
@@ -139,7 +186,7 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
             uint32_t x[4];
             const uint8_t* p = shard_ptr<ADDR>(a, b, as_const(a.in_idx)[c]) + off;
             unpack(vec ? ld16<0>(p) : load_bytes(p, nb), x);
-            madd<MR, 4>(x, [&](int r) { return as_const(a.tables) + (static_cast<uint32_t>(r) * a.k + c) * 5; },
+            madd<MR, 4>(Groups<4>(x), [&](int r) { return as_const(a.tables) + (static_cast<uint32_t>(r) * a.k + c) * 5; },
                         acc, nr);
         }
 #pragma unroll
@@ -200,21 +247,42 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
                 for (int u = 0; u < U; ++u) x[c][u] = ld16<NT>(p + u * kStep);
             }
 #pragma unroll
-            for (int c = 0; c < K; ++c) {
+            for (int c = 0; c + 1 < K; c += 2) {
+                uint32_t xa[NV], xb[NV];
+#pragma unroll
+                for (int u = 0; u < U; ++u) { unpack(x[c][u], xa + 4 * u); unpack(x[c + 1][u], xb + 4 * u); }
+                madd2<MR, NV>(Groups<NV>(xa), [&](int r) { return tables + (r * K + c) * 5; },
+                              Groups<NV>(xb), [&](int r) { return tables + (r * K + c + 1) * 5; }, acc, nr);
+            }
+            if constexpr (K & 1) {
                 uint32_t xv[NV];
 #pragma unroll
-                for (int u = 0; u < U; ++u) unpack(x[c][u], xv + 4 * u);
-                madd<MR, NV>(xv, [&](int r) { return tables + (r * K + c) * 5; }, acc, nr);
+                for (int u = 0; u < U; ++u) unpack(x[K - 1][u], xv + 4 * u);
+                madd<MR, NV>(Groups<NV>(xv), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, nr);
             }
         } else {
             const int k = a.k;
-#pragma unroll 2
-            for (int c = 0; c < k; ++c) {
+            int c = 0;
+            for (; c + 1 < k; c += 2) {
+                const uint8_t* pa = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
+                const uint8_t* pb = shard_ptr<ADDR>(a, b, in_idx[c + 1]) + lane_off;
+                uint32_t xa[NV], xb[NV];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    unpack(ld16<NT>(pa + u * kStep), xa + 4 * u);
+                    unpack(ld16<NT>(pb + u * kStep), xb + 4 * u);
+                }
+                madd2<MR, NV>(Groups<NV>(xa), [&](int r) { return tables + (static_cast<uint32_t>(r) * k + c) * 5; },
+                              Groups<NV>(xb), [&](int r) { return tables + (static_cast<uint32_t>(r) * k + c + 1) * 5; },
+                              acc, nr);
+            }
+            if (c < k) {
                 const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
                 uint32_t xv[NV];
 #pragma unroll
                 for (int u = 0; u < U; ++u) unpack(ld16<NT>(p + u * kStep), xv + 4 * u);
-                madd<MR, NV>(xv, [&](int r) { return tables + (static_cast<uint32_t>(r) * k + c) * 5; }, acc, nr);
+                madd<MR, NV>(Groups<NV>(xv), [&](int r) { return tables + (static_cast<uint32_t>(r) * k + c) * 5; },
+                             acc, nr);
             }
         }
 

@@ -225,7 +225,7 @@ def test_client_degraded_read_like_TestRSRecovery(off, length):
     from blb_amd import reedsolomon
     n, m, target = 6, 3, 2
     rng = np.random.default_rng(off)
-    S = TRACT_LENGTH
+    S = max(TRACT_LENGTH, off + length + 4096)  # RS pieces hold several packed tracts
     shards = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(n)] + [np.empty(S, np.uint8) for _ in range(m)]
     reedsolomon.New(n, m).Encode(shards)
     pieces = {f"ts{i}": shards[i] for i in range(n + m)}
