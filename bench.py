@@ -169,6 +169,20 @@ def main():
             "GiBps_data": round(B * k * S / GIB / (dec_ms * 1e-3), 2),
             "ms_per_launch": round(dec_ms, 3),
             "hbm_GBps_algorithmic": round(B * (k + 1) * S / (dec_ms * 1e-3) / 1e9, 1)}
+        # Verify (reconstructAndVerify's parity recompute + compare, store.go:1136), fused.
+        ver_evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(max(3, a.steps // 2))]
+        flags_ok = True
+        for s, e in ver_evs:
+            s.record(stream)
+            okv = enc.VerifyBatch(stripes)
+            e.record(stream)
+            flags_ok = flags_ok and bool(okv.all())
+        torch.cuda.synchronize(dev)
+        ver_ms = float(np.mean([s.elapsed_time(e) for s, e in ver_evs]))
+        extra["verify"] = {"GiBps_data": round(B * k * S / GIB / (ver_ms * 1e-3), 2),
+                           "ms_per_launch": round(ver_ms, 3), "all_ok": flags_ok,
+                           "hbm_GBps_algorithmic": round(B * (k + m) * S / (ver_ms * 1e-3) / 1e9, 1)}
         # BASELINE config 5 shape on one GPU: PCIe-inclusive streaming from pinned host.
         nb = 16
         pinned = torch.empty((nb, k + m, S), dtype=torch.uint8).pin_memory()

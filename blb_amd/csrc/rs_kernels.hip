@@ -171,6 +171,14 @@ __device__ __forceinline__ bool neq(const V4& a, const V4& b) {
     return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) != 0u;
 }
 
+// Verify: at most one atomic per wave (the lowest lane with a mismatch), so a batch of
+// bad stripes does not serialise every lane on one flag word.
+__device__ __forceinline__ void flag_mismatch(int32_t* flag, bool bad) {
+    const unsigned long long m = __ballot(bad);
+    if (m != 0ull && (threadIdx.x & 63u) == static_cast<unsigned>(__ffsll(static_cast<long long>(m)) - 1))
+        atomicOr(flag, 1);
+}
+
 // Partial / unaligned tiles (runtime k, rows <= MR): 16-byte vector accesses where a
 // chunk is whole and aligned, byte accesses for the shard's ragged end or unaligned shards.
 template <int MR, int MODE, int ADDR, int U>
@@ -238,6 +246,20 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
         constexpr uint32_t kStep = kThreads * kBytesPerThread;
         uint32_t acc[MR][NV] = {};
 
+        // Verify: the shards to check are loaded up front with the inputs, so the whole
+        // tile's reads are in flight before any math.
+        V4 chk[MODE == 1 ? MR : 1][U];
+        if constexpr (MODE == 1) {
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                if (r < nr) {
+                    const uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) chk[r][u] = ld16<NT>(q + u * kStep);
+                }
+            }
+        }
+
         if constexpr (K > 0) {
             V4 x[K][U];
 #pragma unroll
@@ -296,9 +318,8 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
             } else {
                 bool bad = false;
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    bad |= neq(ld16<NT>(q + u * kStep), pack(acc[r] + 4 * u));
-                if (bad) atomicOr(&a.mismatch[b], 1);
+                for (int u = 0; u < U; ++u) bad |= neq(chk[r][u], pack(acc[r] + 4 * u));
+                flag_mismatch(a.mismatch + b, bad);
             }
         }
     }
@@ -314,15 +335,17 @@ constexpr int kMaxTemplRows = 5;
 
 // Launch policy, measured on MI355X (tools/tune_kernels.hip, profiles/r01/tune*.txt):
 //  * nontemporal loads and stores (every byte is touched once): +2-5 %;
-//  * U = 4 chunks per lane (16 KiB tiles) when the K*U + MR*U dwordx4 registers fit
-//    (K + MR <= 11), else U = 2 -- RS(10,4)/RS(12,5) at U = 4 hit 256 VGPRs and halve;
+//  * store mode: U = 4 chunks per lane (16 KiB tiles) when K + MR <= 9, else U = 2 -- wider
+//    shapes at U = 4 drop to one wave per SIMD (RS(10,4) 4.6 vs 6.2 TB/s);
+//  * verify mode (check shards prefetched with the inputs): U = 2 -- 6.8 TB/s, faster than
+//    a plain 9-shard read stream; U = 4 needs too many VGPRs;
 //  * one tile per block in dispatch order (no persistent grid-stride), with each XCD given
 //    a contiguous eighth of the tiles: +10-16 % over a resident persistent grid.
 constexpr int kNT = 3;
-constexpr int pick_u(int K, int MR) { return (K > 0 && K + MR <= 11) ? 4 : 2; }
+constexpr int pick_u(int K, int MR, int MODE) { return (MODE == 0 && K > 0 && K + MR <= 9) ? 4 : 2; }
 
 template <int K, int MR, int MODE, int ADDR>
-constexpr KernelFn fn_of() { return rs_code_kernel<K, MR, MODE, ADDR, pick_u(K, MR), kNT>; }
+constexpr KernelFn fn_of() { return rs_code_kernel<K, MR, MODE, ADDR, pick_u(K, MR, MODE), kNT>; }
 
 struct Choice {
     KernelFn fn = nullptr;
@@ -333,14 +356,14 @@ struct Choice {
 template <int K, int MODE, int ADDR>
 Choice pick_rows(int rows) {
     switch (rows) {
-        case 1: return {fn_of<K, 1, MODE, ADDR>(), pick_u(K, 1), K > 0};
-        case 2: return {fn_of<K, 2, MODE, ADDR>(), pick_u(K, 2), K > 0};
-        case 3: return {fn_of<K, 3, MODE, ADDR>(), pick_u(K, 3), K > 0};
-        case 4: return {fn_of<K, 4, MODE, ADDR>(), pick_u(K, 4), K > 0};
-        case 5: return {fn_of<K, 5, MODE, ADDR>(), pick_u(K, 5), K > 0};
-        case 6: return {fn_of<0, 6, MODE, ADDR>(), pick_u(0, 6), false};
-        case 7: return {fn_of<0, 7, MODE, ADDR>(), pick_u(0, 7), false};
-        case 8: return {fn_of<0, 8, MODE, ADDR>(), pick_u(0, 8), false};
+        case 1: return {fn_of<K, 1, MODE, ADDR>(), pick_u(K, 1, MODE), K > 0};
+        case 2: return {fn_of<K, 2, MODE, ADDR>(), pick_u(K, 2, MODE), K > 0};
+        case 3: return {fn_of<K, 3, MODE, ADDR>(), pick_u(K, 3, MODE), K > 0};
+        case 4: return {fn_of<K, 4, MODE, ADDR>(), pick_u(K, 4, MODE), K > 0};
+        case 5: return {fn_of<K, 5, MODE, ADDR>(), pick_u(K, 5, MODE), K > 0};
+        case 6: return {fn_of<0, 6, MODE, ADDR>(), pick_u(0, 6, MODE), false};
+        case 7: return {fn_of<0, 7, MODE, ADDR>(), pick_u(0, 7, MODE), false};
+        case 8: return {fn_of<0, 8, MODE, ADDR>(), pick_u(0, 8, MODE), false};
         default: return {};
     }
 }
