@@ -373,3 +373,47 @@ def test_baseline_rs104_b512_two_erasures(oracle_lib, dev):
     assert bool(enc.VerifyBatch(st).all())
     del st
     torch.cuda.empty_cache()
+
+
+def _pinned(a):
+    return torch.from_numpy(a).pin_memory().numpy()
+
+
+def test_zero_copy_pinned_host_calls(oracle_lib):
+    """Pinned host shards take the zero-copy path (the kernel reads/writes host memory in
+    place over PCIe); results must match the staged (pageable) path and the oracle."""
+    for k, m, S in [(6, 3, 1 << 20), (10, 4, 12345), (3, 2, 1)]:
+        rng = np.random.default_rng(S)
+        data = rand_shards(rng, k, S)
+        want = oracle_encode(oracle_lib, k, m, data)
+        enc = rs.New(k, m)
+        sh = [_pinned(d.copy()) for d in data] + [_pinned(np.full(S, 0x3C, np.uint8)) for _ in range(m)]
+        enc.Encode(sh)
+        for j in range(m):
+            assert np.array_equal(sh[k + j], want[j]), (k, m, S, j)
+        assert enc.Verify(sh)
+        sh[k][S // 2] ^= 0x40
+        assert not enc.Verify(sh)
+        sh[k][S // 2] ^= 0x40
+        full = [s.copy() for s in sh]
+        lost = [0, k] if m > 1 else [0]
+        cur = [None if i in lost else sh[i] for i in range(k + m)]
+        out0 = _pinned(np.zeros(S + 64, np.uint8))
+        enc.Reconstruct(cur, outs={0: out0})   # pinned output buffer -> zero-copy
+        for i in range(k + m):
+            assert np.array_equal(cur[i], full[i]), (k, m, S, i)
+        assert cur[0].ctypes.data == out0.ctypes.data
+
+
+def test_streaming_host_batch_pageable_fallback(oracle_lib):
+    """Pageable stripes cannot be mapped: the batch takes the H2D/kernel/D2H pipeline."""
+    k, m, S, B = 6, 3, 300001, 5
+    enc = rs.New(k, m)
+    rng = np.random.default_rng(4)
+    stripes = [[rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+               for _ in range(B)]
+    enc.EncodeHostBatch(stripes, nstreams=2)
+    for st in stripes:
+        want = oracle_encode(oracle_lib, k, m, st[:k])
+        for j in range(m):
+            assert np.array_equal(st[k + j], want[j])

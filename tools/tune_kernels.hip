@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -110,7 +111,45 @@ void run_rs(CodeArgs a, int grid, const char* tag, int remap = 0) {
            double(a.B) * kk * S / (ms * 1e-3) / double(1u << 30));
 }
 
+// Zero-copy: the coding kernel reads/writes pinned host stripes directly over PCIe.
+static void zero_copy_probe() {
+    const uint32_t nb = 24;
+    const size_t bytes = size_t(nb) * 9 * S;
+    for (unsigned flags : {0u /*default*/, 0x40000000u /*hipHostMallocNonCoherent*/}) {
+        uint8_t* h = nullptr;
+        if (hipHostMalloc(&h, bytes, flags) != hipSuccess) { printf("hostmalloc %x failed\n", flags); continue; }
+        memset(h, 0x37, bytes);
+        std::vector<uint32_t> tab(6 * 3 * 5, 0x03020100u);
+        int32_t idx[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8};
+        uint32_t* d_tab; int32_t* d_idx;
+        CK(hipMalloc(&d_tab, tab.size() * 4));
+        CK(hipMalloc(&d_idx, sizeof(idx)));
+        CK(hipMemcpy(d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_idx, idx, sizeof(idx), hipMemcpyHostToDevice));
+        CodeArgs c{};
+        c.tables = d_tab; c.in_idx = d_idx; c.out_idx = d_idx + 6; c.base = h;
+        c.shard_stride = S; c.stripe_stride = 9 * S; c.B = nb; c.S = S; c.k = 6; c.rows = 3; c.aligned = 1;
+        for (int u : {2, 4}) {
+            c.tiles_per_stripe = static_cast<uint32_t>(S / (4096 * u));
+            const uint32_t total = nb * c.tiles_per_stripe;
+            for (int grid : {1024, 4096, static_cast<int>(total & ~7u)}) {
+                c.xcd_remap = 1;
+                double ms = time_ms([&] {
+                    if (u == 4) hipLaunchKernelGGL((rs_code_kernel<6, 3, 0, 0, 4, 3>), dim3(grid), dim3(256), 0, 0, c);
+                    else hipLaunchKernelGGL((rs_code_kernel<6, 3, 0, 0, 2, 3>), dim3(grid), dim3(256), 0, 0, c);
+                }, 3);
+                printf("zero-copy flags=%x U=%d grid=%7d : %8.3f ms  %6.2f GiB/s data  (%5.1f GB/s rd, %5.1f GB/s wr)\n",
+                       flags, u, grid, ms, double(nb) * 6 * S / (ms * 1e-3) / double(1u << 30),
+                       double(nb) * 6 * S / ms / 1e6, double(nb) * 3 * S / ms / 1e6);
+            }
+        }
+        CK(hipHostFree(h));
+        CK(hipFree(d_tab)); CK(hipFree(d_idx));
+    }
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "zc") { zero_copy_probe(); return 0; }
     const bool pmc = argc > 1 && std::string(argv[1]) == "pmc";
     if (argc > 1 && !pmc) B = static_cast<uint32_t>(atoi(argv[1]));
     const size_t total = size_t(B) * 9 * S;
