@@ -1,0 +1,81 @@
+// core.hpp -- the slice of blb's internal/core the RS path touches (C++ restatement).
+#pragma once
+#include <cstdint>
+#include <string>
+
+namespace core {
+
+constexpr int64_t TractLength = 8 * 1024 * 1024;                   // constants.go:15
+constexpr int RSChunkVersion = -317866832;                         // constants.go:36
+constexpr int64_t RSPieceLength = 64 * 1024 * 1024 - 64 * 1024 - 64;  // curator/storage_class_loop.go:22
+constexpr uint64_t MaxRSChunkKey = (uint64_t{1} << 48) - 1;        // ids.go
+
+// core.Error values on the RS path (internal/core/errors.go).
+enum class Error {
+    NoError,
+    ErrVersionMismatch,
+    ErrShortRead,
+    ErrCorruptData,
+    ErrEOF,
+    ErrInvalidArgument,
+    ErrHostNotExist,
+    ErrRPC,
+    ErrUnknown,
+    ErrAllocHost,
+};
+
+inline const char* String(Error e) {
+    switch (e) {
+        case Error::NoError: return "no error";
+        case Error::ErrVersionMismatch: return "version mismatch";
+        case Error::ErrShortRead: return "short read";
+        case Error::ErrCorruptData: return "corrupt data";
+        case Error::ErrEOF: return "EOF";
+        case Error::ErrInvalidArgument: return "invalid argument";
+        case Error::ErrHostNotExist: return "host does not exist";
+        case Error::ErrRPC: return "rpc error";
+        case Error::ErrUnknown: return "unknown error";
+        case Error::ErrAllocHost: return "could not allocate host";
+    }
+    return "?";
+}
+
+struct TractID {
+    uint64_t Blob = 0;
+    uint16_t Index = 0;
+    bool operator==(const TractID& o) const { return Blob == o.Blob && Index == o.Index; }
+};
+
+// ids.go:113 -- RS partitions have upper two bits 10.
+struct RSChunkID {
+    uint32_t Partition = 0;
+    uint64_t ID = 0;
+    bool IsValid() const {
+        return (Partition & 0x3fffffffu) != 0 && (Partition >> 30) == 2 && ID != 0 && ID <= MaxRSChunkKey;
+    }
+    RSChunkID Add(int i) const { return RSChunkID{Partition, ID + static_cast<uint64_t>(i)}; }
+    TractID ToTractID() const {
+        return TractID{(static_cast<uint64_t>(Partition) << 32) | ((ID >> 16) & 0xffffffffull),
+                       static_cast<uint16_t>(ID & 0xffff)};
+    }
+};
+
+struct TSAddr {
+    uint64_t ID = 0;
+    std::string Host;
+};
+
+// internal/core/StorageClass.go:7-13 and storageclass.go RSParams.
+enum class StorageClass : int32_t { REPLICATED = 0, RS_6_3 = 1, RS_8_3 = 2, RS_10_3 = 3, RS_12_5 = 4 };
+
+inline bool RSParams(StorageClass c, int* n, int* m) {
+    switch (c) {
+        case StorageClass::RS_6_3: *n = 6; *m = 3; return true;
+        case StorageClass::RS_8_3: *n = 8; *m = 3; return true;
+        case StorageClass::RS_10_3: *n = 10; *m = 3; return true;
+        case StorageClass::RS_12_5: *n = 12; *m = 5; return true;
+        default: return false;
+    }
+}
+
+}  // namespace core

@@ -1,0 +1,336 @@
+// rs_test.cpp -- blb's RS tests, ported to the C++ mirror over the MI355X engine.
+//
+// TestRSEncode / TestRSReconstruct follow internal/tractserver/store_test.go:749-879 line
+// for line (memTractserverTalker with scripted replies, RS(3,2), B=12000 in 5000-byte
+// increments / B=20000 with pieces 1 and 3 missing and indexMap [0,2,4,1,3]), checked with
+// the engine's Verify exactly as the Go test uses enc.Verify.  TestClientRecovery follows
+// internal/testblb/test_rs_recovery.go's reads after a tractserver dies.
+//
+// usage: rs_test [--cpu]   (--cpu: only the tests that need no GPU)
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../blb_amd/host/client.hpp"
+#include "../../blb_amd/host/reedsolomon.hpp"
+#include "../../blb_amd/host/tractserver.hpp"
+
+using blb::Bytes;
+using core::Error;
+
+// ---- a minimal testing.T ----
+struct T {
+    std::string name;
+    bool failed = false;
+    void Errorf(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+};
+void T::Errorf(const char* fmt, ...) {
+    failed = true;
+    va_list ap;
+    va_start(ap, fmt);
+    std::fprintf(stderr, "    %s: ", name.c_str());
+    std::vfprintf(stderr, fmt, ap);
+    std::fprintf(stderr, "\n");
+    va_end(ap);
+}
+#define Fatalf(...) do { t->Errorf(__VA_ARGS__); return; } while (0)
+
+static Bytes randBytes(std::mt19937_64& rng, size_t n) {
+    Bytes b = Bytes::make(n);
+    for (size_t i = 0; i < n; ++i) b[i] = static_cast<uint8_t>(rng());
+    return b;
+}
+
+static Bytes concat(const Bytes& a, const Bytes& b) {
+    Bytes c = Bytes::make(a.len() + b.len());
+    if (a.len()) std::memcpy(c.data(), a.data(), a.len());
+    if (b.len()) std::memcpy(c.data() + a.len(), b.data(), b.len());
+    return c;
+}
+
+// store_test.go:21-81
+struct ReadReply { Bytes B; Error Err; };
+struct WriteReq { core::TractID ID; int Version; Bytes B; int64_t Off; };
+
+class memTractserverTalker : public tractserver::TractserverTalker {
+ public:
+    std::mutex mu;
+    std::map<std::string, std::vector<ReadReply>> ctlReadReplies;
+    std::map<std::string, std::vector<Error>> ctlWriteReplies;
+    std::map<std::string, std::vector<WriteReq>> ctlWriteCalls;
+    std::map<std::string, int> ctlReadCalls;
+
+    void addCtlReadReply(const std::string& addr, const Bytes& origB, Error err) {
+        std::lock_guard<std::mutex> g(mu);
+        ctlReadReplies[addr].push_back({Bytes::copy_of(origB.data(), origB.len()), err});
+    }
+    void addCtlWriteReply(const std::string& addr, Error err) {
+        std::lock_guard<std::mutex> g(mu);
+        ctlWriteReplies[addr].push_back(err);
+    }
+    std::pair<Bytes, Error> CtlRead(const std::string& addr, core::TractID, int, int, int64_t) override {
+        std::lock_guard<std::mutex> g(mu);
+        ctlReadCalls[addr]++;
+        auto& q = ctlReadReplies[addr];
+        if (q.empty()) return {Bytes(), Error::ErrRPC};
+        ReadReply r = q.front();
+        q.erase(q.begin());
+        return {r.B, r.Err};
+    }
+    Error CtlWrite(const std::string& addr, core::TractID id, int v, int64_t off, const Bytes& b) override {
+        std::lock_guard<std::mutex> g(mu);
+        ctlWriteCalls[addr].push_back({id, v, Bytes::copy_of(b.data(), b.len()), off});
+        auto& q = ctlWriteReplies[addr];
+        if (q.empty()) return Error::ErrRPC;
+        Error e = q.front();
+        q.erase(q.begin());
+        return e;
+    }
+};
+
+static std::vector<core::TSAddr> makeAddrs(int n) {
+    std::vector<core::TSAddr> a(n);
+    for (int i = 0; i < n; ++i) a[i] = core::TSAddr{static_cast<uint64_t>(i), "addr" + std::to_string(i)};
+    return a;
+}
+
+static const core::RSChunkID cid{0x80000005u, 5000};
+
+// ---------------------------------------------------------------- CPU-only tests
+
+static void TestNewErrors(T* t) {
+    auto [e0, err0] = reedsolomon::New(0, 3);
+    if (e0 || err0 != reedsolomon::Err::ErrInvShardNum) Fatalf("New(0,3): %s", reedsolomon::ErrString(err0));
+    auto [e1, err1] = reedsolomon::New(6, 0);
+    if (e1 || err1 != reedsolomon::Err::ErrInvShardNum) Fatalf("New(6,0): %s", reedsolomon::ErrString(err1));
+    auto [e2, err2] = reedsolomon::New(250, 7);
+    if (e2 || err2 != reedsolomon::Err::ErrMaxShardNum) Fatalf("New(250,7): %s", reedsolomon::ErrString(err2));
+    auto [e3, err3] = reedsolomon::New(250, 6);
+    if (!e3 || err3 != reedsolomon::Err::None) Fatalf("New(250,6) failed");
+}
+
+static void TestShardChecks(T* t) {
+    auto [enc, err] = reedsolomon::New(3, 2);
+    reedsolomon::Shards four(4, Bytes::make(10));
+    if (enc->Encode(four) != reedsolomon::Err::ErrTooFewShards) Fatalf("want ErrTooFewShards");
+    reedsolomon::Shards empty(5);
+    if (enc->Encode(empty) != reedsolomon::Err::ErrShardNoData) Fatalf("want ErrShardNoData");
+    reedsolomon::Shards ragged{Bytes::make(10), Bytes::make(10), Bytes::make(9), Bytes::make(10), Bytes::make(10)};
+    if (enc->Encode(ragged) != reedsolomon::Err::ErrShardSize) Fatalf("want ErrShardSize");
+    reedsolomon::Shards few{Bytes::make(10), Bytes(), Bytes(), Bytes(), Bytes::make(10)};
+    if (enc->Reconstruct(few) != reedsolomon::Err::ErrTooFewShards) Fatalf("want ErrTooFewShards");
+    reedsolomon::Shards all(5, Bytes::make(10));
+    if (enc->Reconstruct(all) != reedsolomon::Err::None) Fatalf("all present must be a no-op");
+}
+
+static void TestRSEncodeArgErrors(T* t) {
+    memTractserverTalker tt;
+    tractserver::Store s(&tt, tractserver::Config{5000, false});
+    auto addrs = makeAddrs(5);
+    std::vector<core::TSAddr> srcs(addrs.begin(), addrs.begin() + 3), dests(addrs.begin() + 3, addrs.end());
+    if (s.RSEncode(core::RSChunkID{5, 5000}, 12000, srcs, dests, {}) != Error::ErrInvalidArgument)
+        Fatalf("non-RS partition accepted");
+    if (s.RSEncode(cid, 12000, srcs, dests, {0, 1, 2}) != Error::ErrInvalidArgument) Fatalf("bad indexMap accepted");
+    // no replies scripted: the first CtlRead fails with ErrRPC before any coding
+    if (s.RSEncode(cid, 12000, srcs, dests, {}) != Error::ErrRPC) Fatalf("want ErrRPC");
+}
+
+// ---------------------------------------------------------------- GPU tests
+
+// store_test.go:749-815
+static void TestRSEncode(T* t, bool pipeline) {
+    const int N = 3, M = 2, B = 12000;
+    memTractserverTalker tt;
+    tractserver::Store s(&tt, tractserver::Config{5000, pipeline});
+    auto addrs = makeAddrs(N + M);
+    std::mt19937_64 rng(97531);
+    std::vector<Bytes> data(N + M);
+    for (int i = 0; i < N; ++i) data[i] = randBytes(rng, B);
+
+    const int cuts[4] = {0, 5000, 10000, 12000};  // 0..5000, 5000..10000, 10000..12000
+    for (int w = 0; w < 3; ++w) {
+        for (int i = 0; i < N; ++i) tt.addCtlReadReply(addrs[i].Host, data[i].slice(cuts[w], cuts[w + 1]), Error::ErrEOF);
+        for (int i = N; i < N + M; ++i) tt.addCtlWriteReply(addrs[i].Host, Error::NoError);
+    }
+    std::vector<core::TSAddr> srcs(addrs.begin(), addrs.begin() + N), dests(addrs.begin() + N, addrs.end());
+    Error err = s.RSEncode(cid, B, srcs, dests, {});
+    if (err != Error::NoError) Fatalf("error from RSEncode: %s", core::String(err));
+
+    for (int i = N; i < N + M; ++i) {
+        int j = 0;
+        for (const auto& reply : tt.ctlWriteCalls[addrs[i].Host]) {
+            if (!(reply.ID == cid.Add(i).ToTractID())) t->Errorf("bad tract id for reply %d from %d", j, i);
+            if (reply.Off != static_cast<int64_t>(data[i].len()))
+                t->Errorf("bad offset for reply %d from %d: %lld != %zu", j, i, (long long)reply.Off, data[i].len());
+            data[i] = concat(data[i], reply.B);
+            ++j;
+        }
+    }
+    auto [enc, e] = reedsolomon::New(N, M);
+    auto [ok, verr] = enc->Verify(data);
+    if (verr != reedsolomon::Err::None || !ok) Fatalf("RS verify failed: %s, %d", reedsolomon::ErrString(verr), ok);
+}
+
+// store_test.go:817-879
+static void TestRSReconstruct(T* t, bool pipeline) {
+    const int N = 3, M = 2, B = 20000;
+    memTractserverTalker tt;
+    tractserver::Store s(&tt, tractserver::Config{1 << 20, pipeline});
+    auto addrs = makeAddrs(N + M);
+    std::mt19937_64 rng(97532);
+    std::vector<Bytes> data(N + M);
+    for (int i = 0; i < N + M; ++i) data[i] = randBytes(rng, B);
+
+    auto [enc, e] = reedsolomon::New(N, M);
+    if (enc->Encode(data) != reedsolomon::Err::None) Fatalf("RS encode failed");
+    std::vector<Bytes> want = data;
+
+    // We're missing 1 (data) and 3 (parity): 0_2_4
+    data[1] = Bytes();
+    data[3] = Bytes();
+    tt.addCtlReadReply(addrs[0].Host, data[0], Error::ErrEOF);
+    tt.addCtlReadReply(addrs[2].Host, data[2], Error::ErrEOF);
+    tt.addCtlReadReply(addrs[4].Host, data[4], Error::ErrEOF);
+    tt.addCtlWriteReply(addrs[1].Host, Error::NoError);
+    tt.addCtlWriteReply(addrs[3].Host, Error::NoError);
+
+    Error err = s.RSEncode(cid, B, {addrs[0], addrs[2], addrs[4]}, {addrs[1], addrs[3]}, {0, 2, 4, 1, 3});
+    if (err != Error::NoError) Fatalf("error from RSEncode: %s", core::String(err));
+    for (int i : {1, 3}) {
+        for (const auto& reply : tt.ctlWriteCalls[addrs[i].Host]) {
+            if (!(reply.ID == cid.Add(i).ToTractID())) t->Errorf("bad tract id from %d", i);
+            if (reply.Off != static_cast<int64_t>(data[i].len())) t->Errorf("bad offset from %d", i);
+            data[i] = concat(data[i], reply.B);
+        }
+    }
+    auto [ok, verr] = enc->Verify(data);
+    if (verr != reedsolomon::Err::None || !ok) Fatalf("RS verify failed");
+    for (int i = 0; i < N + M; ++i)
+        if (!data[i].equal(want[i])) Fatalf("piece %d differs from the original", i);
+}
+
+// Cap reuse: a missing shard with room gets the output in its own backing array
+// (client/blb/reconstruct.go:172-175).
+static void TestReconstructDataIntoCallerBuffer(T* t) {
+    const int n = 6, m = 3, L = 98765;
+    std::mt19937_64 rng(5);
+    auto [enc, e] = reedsolomon::New(n, m);
+    reedsolomon::Shards sh(n + m);
+    for (int i = 0; i < n; ++i) sh[i] = randBytes(rng, L);
+    for (int i = n; i < n + m; ++i) sh[i] = Bytes::make(L);
+    if (enc->Encode(sh) != reedsolomon::Err::None) Fatalf("encode");
+    Bytes truth = Bytes::copy_of(sh[2].data(), L);
+    Bytes thisB = Bytes::make(L + 5);
+    sh[2] = thisB.slice3(0, 0, L);
+    sh[7] = Bytes();
+    if (enc->ReconstructData(sh) != reedsolomon::Err::None) Fatalf("ReconstructData");
+    if (sh[2].data() != thisB.data() || sh[2].len() != static_cast<size_t>(L)) Fatalf("output not in caller buffer");
+    if (!sh[2].equal(truth)) Fatalf("wrong bytes");
+    if (sh[7].len() != 0) Fatalf("ReconstructData rebuilt parity");
+}
+
+// test_rs_recovery.go: a tractserver holding a piece dies; reads of that piece are
+// reconstructed from n others into the caller's buffer.
+class memPieces : public client::TractserverTalker {
+ public:
+    std::map<std::string, Bytes> pieces;
+    std::map<std::string, bool> down;
+    std::atomic<int> reads{0};
+    std::pair<Bytes, Error> Read(const std::string& addr, core::TractID, int, int length, int64_t off) override {
+        ++reads;
+        if (down[addr]) return {Bytes(), Error::ErrRPC};
+        const Bytes& p = pieces[addr];
+        const size_t end = std::min<size_t>(p.len(), off + length);
+        return {Bytes::copy_of(p.data() + off, end - off), end == p.len() ? Error::ErrEOF : Error::NoError};
+    }
+    std::pair<int, Error> ReadInto(const std::string& addr, core::TractID, int, Bytes b, int64_t off) override {
+        if (down[addr]) return {0, Error::ErrRPC};
+        const Bytes& p = pieces[addr];
+        const size_t n = std::min<size_t>(b.len(), p.len() - off);
+        std::memcpy(b.data(), p.data() + off, n);
+        return {static_cast<int>(n), Error::NoError};
+    }
+};
+
+static void TestClientRecovery(T* t) {
+    const int n = 6, m = 3, target = 2;
+    const size_t S = core::TractLength + 65536;
+    std::mt19937_64 rng(97531);
+    auto [enc, e] = reedsolomon::New(n, m);
+    reedsolomon::Shards sh(n + m);
+    for (int i = 0; i < n; ++i) sh[i] = randBytes(rng, S);
+    for (int i = n; i < n + m; ++i) sh[i] = Bytes::make(S);
+    if (enc->Encode(sh) != reedsolomon::Err::None) Fatalf("encode");
+    memPieces ts;
+    client::TractPointer tr;
+    tr.Chunk = cid.Add(target);
+    tr.Host = "ts2";
+    tr.TSID = 100 + target;
+    tr.Length = static_cast<uint32_t>(core::TractLength);
+    tr.Class = core::StorageClass::RS_6_3;
+    tr.BaseChunk = cid;
+    for (int i = 0; i < n + m; ++i) {
+        const std::string h = "ts" + std::to_string(i);
+        ts.pieces[h] = sh[i];
+        tr.OtherHosts.push_back(h);
+        tr.OtherTSIDs.push_back(100 + i);
+    }
+    ts.down["ts2"] = true;  // the piece we want
+    ts.down["ts5"] = true;  // and one more
+    client::Client cli(&ts, client::ReconstructBehavior{});
+    // test_rs_recovery.go's windows; the caller (readAt) clips each read to the tract, and
+    // a tract shorter than the buffer reads as EOF with zero padding (client.go:1193-1202).
+    struct Case { int64_t off; int buf; uint32_t tractLen; int want; Error err; };
+    const Case cases[] = {
+        {4000, 123000, static_cast<uint32_t>(core::TractLength), 123000, Error::NoError},
+        {core::TractLength - 56789, 56789, static_cast<uint32_t>(core::TractLength), 56789, Error::NoError},
+        {0, 6000, 5000, 5000, Error::ErrEOF},
+    };
+    for (const Case& c : cases) {
+        Bytes buf = Bytes::make(c.buf);
+        std::memset(buf.data(), 0xEE, c.buf);
+        client::TractPointer tc = tr;
+        tc.Length = c.tractLen;
+        client::TractResult r = cli.readOneTractRS(tc, buf, c.off);
+        if (r.err != c.err || r.read != c.want)
+            Fatalf("read at %lld: %s, %d bytes", (long long)c.off, core::String(r.err), r.read);
+        if (std::memcmp(buf.data(), sh[target].data() + c.off, c.want) != 0) Fatalf("wrong reconstructed bytes");
+        for (int i = c.want; i < c.buf; ++i)
+            if (buf[i] != 0) Fatalf("not zero padded at %d", i);
+    }
+    if (cli.Reconstructs() != 3) Fatalf("want 3 reconstructs, got %d", cli.Reconstructs());
+}
+
+int main(int argc, char** argv) {
+    const bool cpu_only = argc > 1 && std::string(argv[1]) == "--cpu";
+    struct Test { const char* name; void (*fn)(T*); bool gpu; };
+    const Test tests[] = {
+        {"TestNewErrors", TestNewErrors, false},
+        {"TestShardChecks", TestShardChecks, false},
+        {"TestRSEncodeArgErrors", TestRSEncodeArgErrors, false},
+        {"TestRSEncode", [](T* t) { TestRSEncode(t, false); }, true},
+        {"TestRSEncode/pipelined", [](T* t) { TestRSEncode(t, true); }, true},
+        {"TestRSReconstruct", [](T* t) { TestRSReconstruct(t, false); }, true},
+        {"TestRSReconstruct/pipelined", [](T* t) { TestRSReconstruct(t, true); }, true},
+        {"TestReconstructDataIntoCallerBuffer", TestReconstructDataIntoCallerBuffer, true},
+        {"TestClientRecovery", TestClientRecovery, true},
+    };
+    int failed = 0, ran = 0;
+    for (const Test& tc : tests) {
+        if (cpu_only && tc.gpu) continue;
+        T t{tc.name};
+        tc.fn(&t);
+        ++ran;
+        std::printf("--- %s: %s\n", t.failed ? "FAIL" : "PASS", tc.name);
+        failed += t.failed;
+    }
+    std::printf("%s (%d tests, %d failed)\n", failed ? "FAIL" : "PASS", ran, failed);
+    return failed ? 1 : 0;
+}
