@@ -148,10 +148,33 @@ static void zero_copy_probe() {
     }
 }
 
+// Shard / stripe stride padding: do 9 streams exactly 8 MiB apart alias in the HBM
+// channel/bank hash?  Same kernel, same bytes, different layouts.
+static void stride_probe(CodeArgs a) {
+    const size_t cap = size_t(B) * 9 * S;
+    for (int rep = 0; rep < 2; ++rep)
+        for (uint64_t pad : {0ull, 256ull, 4096ull, 65536ull, 1ull << 20, 3ull << 12}) {
+            for (int mode = 0; mode < 2; ++mode) {  // 0: pad shards, 1: pad stripes only
+                CodeArgs c = a;
+                c.shard_stride = mode == 0 ? S + pad : S;
+                c.stripe_stride = mode == 0 ? 9 * (S + pad) : 9 * S + pad;
+                c.B = static_cast<uint32_t>((cap - 9 * (S + pad)) / c.stripe_stride);
+                if (c.B > 1000) c.B = 1000;
+                c.tiles_per_stripe = static_cast<uint32_t>(S / 16384);
+                c.xcd_remap = 1;
+                const int grid = static_cast<int>(c.B * c.tiles_per_stripe) & ~7;
+                double ms = time_ms([&] { hipLaunchKernelGGL((rs_code_kernel<6, 3, 0, 0, 4, 3>), dim3(grid), dim3(256), 0, 0, c); });
+                printf("stride pad=%8llu %s B=%u : %8.3f ms  %7.1f GB/s\n", (unsigned long long)pad,
+                       mode == 0 ? "shard " : "stripe", c.B, ms, double(c.B) * 9 * S / ms / 1e6);
+            }
+        }
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "zc") { zero_copy_probe(); return 0; }
+    const bool stride = argc > 1 && std::string(argv[1]) == "stride";
     const bool pmc = argc > 1 && std::string(argv[1]) == "pmc";
-    if (argc > 1 && !pmc) B = static_cast<uint32_t>(atoi(argv[1]));
+    if (argc > 1 && !pmc && !stride) B = static_cast<uint32_t>(atoi(argv[1]));
     const size_t total = size_t(B) * 9 * S;
     CK(hipMalloc(&g_base, total));
     CK(hipMalloc(&g_sink, 64));
@@ -184,6 +207,7 @@ int main(int argc, char** argv) {
     };
 
     printf("# B=%u stripes x 9 shards x 8 MiB = %.1f GiB\n", B, total / double(1ull << 30));
+    if (stride) { stride_probe(a); return 0; }
     if (pmc) {
         // Counter calibration (one launch each, run under rocprofv3 --pmc):
         //   pattern R=9 W=0: reads exactly B*9*S bytes, writes nothing;
