@@ -183,6 +183,22 @@ def main():
         extra["verify"] = {"GiBps_data": round(B * k * S / GIB / (ver_ms * 1e-3), 2),
                            "ms_per_launch": round(ver_ms, 3), "all_ok": flags_ok,
                            "hbm_GBps_algorithmic": round(B * (k + m) * S / (ver_ms * 1e-3) / 1e9, 1)}
+        # CRC-32C of every parity shard in 65532-byte ChecksumFile blocks (§8f row 2).
+        from blb_amd import checksum
+        # Parity rows are strided (k+m)*S apart: checksum them as m strided batches of B rows.
+        crc_evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        views = [stripes[:, k + j, :] for j in range(m)]
+        for v in views:
+            checksum.ChecksumBatch(v, checksum.CHECKSUM_BLOCK_DATA)
+        torch.cuda.synchronize(dev)
+        crc_evs[0].record(stream)
+        for v in views:
+            checksum.ChecksumBatch(v, checksum.CHECKSUM_BLOCK_DATA)
+        crc_evs[1].record(stream)
+        torch.cuda.synchronize(dev)
+        crc_ms = crc_evs[0].elapsed_time(crc_evs[1])
+        extra["crc32c_parity_blocks"] = {"GBps": round(B * m * S / (crc_ms * 1e-3) / 1e9, 1),
+                                         "ms": round(crc_ms, 3), "bytes": B * m * S, "block": 65532}
         # BASELINE config 5 shape on one GPU: PCIe-inclusive streaming from pinned host.
         nb = 16
         pinned = torch.empty((nb, k + m, S), dtype=torch.uint8).pin_memory()

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/blb_rs.h"
+#include "crc32c.hpp"
 #include "gf256.hpp"
 #include "rs_kernels.hpp"
 
@@ -850,6 +851,50 @@ int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size
     }
     cleanup();
     return rc;
+}
+
+// ---- CRC-32C ----
+
+int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block,
+                     uint32_t* out_dev, void* stream) {
+    if (batch == 0 || len == 0) return BLBRS_OK;
+    if (!data || !out_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (batch > 1 && stride < len) return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than length");
+    int dev = 0;
+    int rc = current_dev_or_fail(&dev);
+    if (rc) return rc;
+    if (block == 0) block = len;
+    hipError_t e = crc32c_blocks(data, stride, batch, len, block, out_dev, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "crc32c_blocks");
+    return BLBRS_OK;
+}
+
+int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {
+    if (!data || !out) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (len == 0) return BLBRS_OK;
+    if (block == 0) block = len;
+    WorkerLease lease;
+    int rc = lease_worker(lease);
+    if (rc) return rc;
+    Worker& w = *lease.w;
+    const size_t nblocks = (len + block - 1) / block;
+    uint64_t view = 0;
+    const uint8_t* src = nullptr;
+    if (device_view(data, &view)) {
+        src = reinterpret_cast<const uint8_t*>(view);  // pinned / device memory: in place
+    } else {
+        if ((rc = w.ensure(round_up(len, 256)))) return rc;
+        HIP_TRY(hipMemcpyAsync(w.dbuf, data, len, hipMemcpyHostToDevice, w.s[0]));
+        src = w.dbuf;
+    }
+    uint32_t* dout = nullptr;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dout), nblocks * 4, w.s[0]));
+    hipError_t e = crc32c_blocks(src, len, 1, len, block, dout, w.s[0]);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, nblocks * 4, hipMemcpyDeviceToHost, w.s[0]);
+    (void)hipFreeAsync(dout, w.s[0]);
+    if (e == hipSuccess) e = hipStreamSynchronize(w.s[0]);
+    if (e != hipSuccess) return hip_fail(e, "crc32c");
+    return BLBRS_OK;
 }
 
 // ---- misc ----

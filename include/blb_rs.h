@@ -121,6 +121,18 @@ int blbrs_verify_dev_ptrs(blbrs_encoder* enc, const uint8_t* const* shard_ptrs, 
 int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch,
                             size_t shard_len, int nstreams);
 
+/* ---- CRC-32C (Castagnoli) of shard blocks ----
+ * blb checksums every shard it writes on this path: ChecksumFile blocks of 65532 data
+ * bytes (pkg/disk/checksum_block.go:18-34,70-80) and bulk RPC frames (pkg/rpc/
+ * bulk_codec.go:47, block = whole buffer).  For each of `batch` buffers (buffer b at
+ * data + b * stride, `len` bytes), out[b * nblocks + j] = crc32.Checksum(block j,
+ * crc32.MakeTable(crc32.Castagnoli)) with nblocks = ceil(len / block); the last block of a
+ * buffer may be short.  block == 0 means one block per buffer. */
+int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block,
+                     uint32_t* out_dev, void* stream);
+/* Host-memory form: one buffer; out (host) has ceil(len / block) entries. */
+int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out);
+
 /* ---- misc ---- */
 int blbrs_set_device(int device);      /* hipSetDevice for the calling thread */
 int blbrs_device_count(int* count);

@@ -60,6 +60,10 @@ def lib() -> ctypes.CDLL:
         L.rso_encode.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int, ctypes.c_int]
         L.rso_verify.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P]
         L.rso_reconstruct.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int]
+        L.rso_crc32c_update.argtypes = [ctypes.c_uint32, P, ctypes.c_size_t]
+        L.rso_crc32c_update.restype = ctypes.c_uint32
+        L.rso_crc32c_blocks.argtypes = [P, ctypes.c_size_t, ctypes.c_size_t, P]
+        L.rso_crc32c_blocks.restype = None
         L.rso_have_avx2.restype = ctypes.c_int
         L.rso_max_threads.restype = ctypes.c_int
         _lib = L
@@ -125,3 +129,18 @@ def reconstruct(k: int, m: int, shards, data_only: bool):
     _check(lib().rso_reconstruct(k, m, ptrs, L, int(data_only)))
     return [bufs[i] if L[i] else (None if shards[i] is None or shards[i].size == 0 else shards[i])
             for i in range(n)]
+
+
+def crc32c(data, crc: int = 0) -> int:
+    """crc32.Update(crc, castagnoliTable, data) (Checksum when crc == 0)."""
+    a = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if isinstance(data, (bytes, bytearray)) else data,
+                             dtype=np.uint8)
+    return int(lib().rso_crc32c_update(crc, a.ctypes.data, a.size))
+
+
+def crc32c_blocks(data: np.ndarray, block: int) -> np.ndarray:
+    a = np.ascontiguousarray(data, dtype=np.uint8)
+    nb = (a.size + block - 1) // block
+    out = np.zeros(max(nb, 1), np.uint32)
+    lib().rso_crc32c_blocks(a.ctypes.data, a.size, block, out.ctypes.data)
+    return out[:nb]

@@ -170,3 +170,13 @@ def reconstruct(k: int, m: int, shards: list[np.ndarray | None], data_only: bool
 def verify(k: int, m: int, shards: list[np.ndarray]) -> bool:
     par = encode(k, m, shards[:k])
     return all(np.array_equal(p, s) for p, s in zip(par, shards[k:]))
+
+
+def crc32c(data: bytes, crc: int = 0) -> int:
+    """Bitwise CRC-32C (reflected polynomial 0x82F63B78), independent of the C table."""
+    crc = ~crc & 0xFFFFFFFF
+    for b in bytes(data):
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
+    return ~crc & 0xFFFFFFFF

@@ -365,3 +365,34 @@ int rso_reconstruct(int k, int m, uint8_t* const* shards, size_t* lens, int data
     free(sub_m); free(dec); free(rows);
     return RSO_OK;
 }
+
+/* ---- CRC-32C (Castagnoli), as Go's hash/crc32 with crc32.MakeTable(crc32.Castagnoli) ----
+ * Used on blb's RS data path by pkg/disk/checksum_block.go:34,70-80 (64 KiB ChecksumFile
+ * blocks: 65532 data bytes + 4-byte CRC) and pkg/rpc/bulk_codec.go:47 (bulk RPC frames).
+ * rso_crc32c_update = crc32.Update(crc, tab, p); Checksum(p) = Update(0, tab, p). */
+static uint32_t crc32c_table[256];
+static int crc32c_ready = 0;
+
+static void crc32c_init(void) {
+    if (crc32c_ready) return;
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int j = 0; j < 8; j++) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+        crc32c_table[i] = c;
+    }
+    crc32c_ready = 1;
+}
+
+uint32_t rso_crc32c_update(uint32_t crc, const uint8_t* p, size_t n) {
+    crc32c_init();
+    crc = ~crc;
+    for (size_t i = 0; i < n; i++) crc = crc32c_table[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+    return ~crc;
+}
+
+/* CRC of each `block`-byte block of p[0:n] (last block may be short). */
+void rso_crc32c_blocks(const uint8_t* p, size_t n, size_t block, uint32_t* out) {
+    size_t j = 0;
+    for (size_t off = 0; off < n; off += block, j++)
+        out[j] = rso_crc32c_update(0, p + off, (n - off < block) ? n - off : block);
+}

@@ -1,0 +1,83 @@
+"""CRC-32C (Castagnoli) of shard blocks: oracle pinning on CPU, GPU kernel bit-exact vs the
+oracle.  The block sizes are blb's: 65532-byte ChecksumFile blocks
+(pkg/disk/checksum_block.go:18-34) and whole-buffer bulk RPC frames (pkg/rpc/bulk_codec.go:47)."""
+import numpy as np
+import pytest
+
+from oracle import rs_numpy as N
+
+CHECK = 0xE3069283  # CRC-32C("123456789"), the standard check value
+
+
+def test_oracle_crc32c_pinned(oracle_lib):
+    assert oracle_lib.crc32c(b"123456789") == CHECK
+    assert N.crc32c(b"123456789") == CHECK
+    assert oracle_lib.crc32c(b"") == 0
+    rng = np.random.default_rng(7)
+    for n in (1, 3, 100, 4099):
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        assert oracle_lib.crc32c(d) == N.crc32c(d.tobytes())
+        # crc32.Update chaining (checksumBlock.append, checksum_block.go:76-80)
+        cut = n // 3
+        assert oracle_lib.crc32c(d[cut:], oracle_lib.crc32c(d[:cut])) == oracle_lib.crc32c(d)
+    blocks = oracle_lib.crc32c_blocks(np.arange(200000, dtype=np.uint32).view(np.uint8), 65532)
+    assert blocks.size == (800000 + 65531) // 65532
+
+
+gpu = pytest.mark.gpu
+
+
+def _torch():
+    return pytest.importorskip("torch")
+
+
+@gpu
+@pytest.mark.parametrize("block", [65532, 0, 4096, 1000, 1, 65536, 1 << 20])
+def test_gpu_crc32c_vs_oracle(oracle_lib, block):
+    from blb_amd import checksum
+    torch = _torch()
+    rng = np.random.default_rng(block + 1)
+    for n in (1, 3, 4, 15, 65532, 65536, 98765, 3 * 65532 + 7, (8 << 20) + 13):
+        if block == 1 and n > 5000:
+            continue
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        want = oracle_lib.crc32c_blocks(d, block or n)
+        got = checksum.Checksum(d, block)                          # host path (staged)
+        assert np.array_equal(got, want), (n, block)
+        t = torch.from_numpy(d).cuda()
+        got_d = checksum.as_uint32(checksum.Checksum(t, block))    # device path
+        assert np.array_equal(got_d, want), (n, block, "dev")
+
+
+@gpu
+def test_gpu_crc32c_unaligned_and_pinned(oracle_lib):
+    from blb_amd import checksum
+    torch = _torch()
+    rng = np.random.default_rng(3)
+    base = rng.integers(0, 256, 300000, dtype=np.uint8)
+    dbase = torch.from_numpy(base).cuda()
+    for off in (1, 2, 3, 5, 16):
+        d = base[off:off + 200000]
+        want = oracle_lib.crc32c_blocks(d, 65532)
+        assert np.array_equal(checksum.as_uint32(checksum.Checksum(dbase[off:off + 200000], 65532)), want), off
+    pinned = torch.from_numpy(base.copy()).pin_memory().numpy()
+    assert np.array_equal(checksum.Checksum(pinned, 65532), oracle_lib.crc32c_blocks(base, 65532))
+
+
+@gpu
+def test_gpu_crc32c_batch_of_parity_shards(oracle_lib):
+    """The use on the RS path: checksum every parity shard of a device-resident batch right
+    after encoding it (ChecksumFile blocks and the whole-shard bulk-frame CRC)."""
+    from blb_amd import checksum, reedsolomon
+    torch = _torch()
+    k, m, B, S = 6, 3, 8, (1 << 20) + 100
+    enc = reedsolomon.New(k, m)
+    st = torch.randint(0, 256, (B, k + m, S), dtype=torch.uint8, device="cuda")
+    enc.EncodeBatch(st)
+    parity = st[:, k:, :].reshape(B * m, S)           # strided rows
+    crc_blocks = checksum.as_uint32(checksum.ChecksumBatch(parity, 65532))
+    crc_whole = checksum.as_uint32(checksum.ChecksumBatch(parity, 0))
+    host = parity.cpu().numpy()
+    for r in range(B * m):
+        assert np.array_equal(crc_blocks[r], oracle_lib.crc32c_blocks(host[r], 65532)), r
+        assert int(crc_whole[r, 0]) == oracle_lib.crc32c(host[r]), r
