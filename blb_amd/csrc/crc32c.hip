@@ -5,10 +5,12 @@
 //     raw(A || B) = S_{|B|} raw(A)  ^  raw(B)          S_n = "feed n zero bytes", a 32x32
 //     crc(M)      = ~( S_{|M|} 0xFFFFFFFF ^ raw(M) )   GF(2) matrix (host-precomputed).
 // Kernel 1 (one workgroup per <= 64 KiB segment): the segment is staged in LDS behind a
-// zero prefix so that 256 lanes each own exactly L bytes (leading zeros do not change
-// raw); every lane runs slicing-by-4 over its chunk with the four 1 KiB tables in LDS (L/4
-// odd: lanes' dword reads hit distinct banks), then lanes are folded pairwise with
-// S_L, S_2L, ..., S_128L -- shuffles inside a wave, LDS across the four waves.
+// zero prefix so that 256 lanes each own exactly L = C*Lc bytes (leading zeros do not
+// change raw).  Each lane runs C = 4 independent slicing-by-4 chains over its C adjacent
+// Lc-byte sub-chunks (4x the LDS-latency tolerance of one chain), with the four 1 KiB
+// tables in LDS and one pad dword per lane region so every chain read hits 64 distinct
+// banks.  Chains fold with S_{3Lc}, S_{2Lc}, S_{Lc}; lanes fold pairwise with S_L, S_2L,
+// ..., S_128L -- shuffles inside a wave, LDS across the four waves.
 // Kernel 2 (one lane per block): folds the block's segments with S_SEG (Horner) and applies
 // the init term.  CRC is computed byte-serially per lane, so this is LDS/VALU work, not
 // a streaming HBM kernel; it runs beside the coding kernel on the data it just wrote.
@@ -28,6 +30,7 @@ constexpr int kPow2 = 48;                // S_{2^i}, i < 48
 // Device constants for one (L, SEG) configuration.
 struct CrcConsts {
     uint32_t table[4][256];     // slicing-by-4 tables
+    uint32_t chain[3][32];      // S_{(3-j) * Lc}: chain j -> end of the lane's region
     uint32_t lvl[8][32];        // S_{L * 2^j}, columns
     uint32_t seg[32];           // S_SEG
     uint32_t pow2[kPow2][32];   // S_{2^i}
@@ -36,27 +39,40 @@ struct CrcConsts {
 using cu32 = const uint32_t __attribute__((address_space(4)))*;
 __device__ __forceinline__ cu32 as_const(const uint32_t* p) { return (cu32)(uintptr_t)p; }
 
-// r -> S r for a column-major 32x32 GF(2) matrix held in constant memory (scalar loads).
+// r -> S r for a column-major 32x32 GF(2) matrix held in constant memory (scalar loads):
+// per bit, a 1-bit sign-extract and one v_bitop3 (out ^ (mask & col), truth table 0x78).
 __device__ __forceinline__ uint32_t apply(cu32 col, uint32_t r) {
     uint32_t out = 0;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) out ^= ((r >> i) & 1u) ? col[i] : 0u;
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t mask = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(r), i, 1));
+        out = __builtin_amdgcn_bitop3_b32(out, mask, col[i], 0x78);
+    }
     return out;
 }
 
 struct SegArgs {
     const uint8_t* data;
     uint64_t stride, len, block, seg;
-    uint32_t nblocks, segs_per_block, L;  // L: bytes per lane (multiple of 4, L/4 odd)
+    uint32_t nblocks, segs_per_block;
     const CrcConsts* c;
     uint32_t* raw;                        // [batch][nblocks][segs_per_block]
 };
 
+constexpr int kChains = 4;                        // independent CRC chains per lane
+constexpr uint32_t kChainDw = 16;                 // dwords per chain (Lc = 64 bytes)
+constexpr uint32_t kLaneDw = kChains * kChainDw;  // 64 dwords = L = 256 bytes per lane
+constexpr uint32_t kLanePitch = kLaneDw + 1;      // +1 pad dword: conflict-free chain reads
+constexpr uint32_t kSegMax = kThreads * kLaneDw * 4;  // 64 KiB
+constexpr size_t kLdsBytes = (1024 + kThreads * kLanePitch + 4) * 4;
+
+__device__ __forceinline__ uint32_t lds_dw(uint32_t v4) { return (v4 / kLaneDw) * kLanePitch + v4 % kLaneDw; }
+
 __global__ __launch_bounds__(kThreads) void crc_segment_kernel(SegArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* tab = lds;              // 4 x 256
-    uint32_t* buf = lds + 1024;       // V = 256 * L bytes
-    uint32_t* wave_v = buf + (a.L / 4) * kThreads;  // 4 slots
+    uint32_t* tab = lds;                          // 4 x 256
+    uint32_t* buf = lds + 1024;                   // 256 lane regions of kLanePitch dwords
+    uint32_t* wave_v = buf + kThreads * kLanePitch;
     const uint32_t tid = threadIdx.x;
 
     const uint32_t g = blockIdx.x;
@@ -71,18 +87,15 @@ __global__ __launch_bounds__(kThreads) void crc_segment_kernel(SegArgs a) {
         return;
     }
     const uint32_t seglen = static_cast<uint32_t>(blk_end - start < a.seg ? blk_end - start : a.seg);
-    const uint32_t V = a.L * kThreads;
-    const uint32_t pad = V - seglen;
+    const uint32_t pad = kSegMax - seglen;        // virtual zero prefix
     const uint8_t* src = a.data + b * a.stride + start;
 
     for (uint32_t i = tid; i < 1024; i += kThreads) tab[i] = a.c->table[i >> 8][i & 255];
-    uint8_t* buf8 = reinterpret_cast<uint8_t*>(buf);
-    for (uint32_t i = tid; i < pad / 4; i += kThreads) buf[i] = 0u;
+    for (uint32_t v4 = tid; v4 < (pad + 3) / 4; v4 += kThreads) buf[lds_dw(v4)] = 0u;
     if ((reinterpret_cast<uintptr_t>(src) & 3u) == 0 && (seglen & 3u) == 0) {
         // 16 loads in flight per lane before any LDS store (a plain loop waits on each).
         const uint32_t* src32 = reinterpret_cast<const uint32_t*>(src);
-        const uint32_t nd = seglen / 4;
-        uint32_t* dst = buf + pad / 4;
+        const uint32_t nd = seglen / 4, base = pad / 4;
         for (uint32_t i0 = tid; i0 < nd; i0 += kThreads * 16) {
             uint32_t v[16];
 #pragma unroll
@@ -93,32 +106,44 @@ __global__ __launch_bounds__(kThreads) void crc_segment_kernel(SegArgs a) {
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 const uint32_t i = i0 + u * kThreads;
-                if (i < nd) dst[i] = v[u];
+                if (i < nd) buf[lds_dw(base + i)] = v[u];
             }
         }
     } else {
-        if (tid < (pad & 3u)) buf8[(pad & ~3u) + tid] = 0;
-        for (uint32_t i = tid; i < seglen; i += kThreads) buf8[pad + i] = src[i];
+        __syncthreads();  // the zeroed dword holding the prefix's last bytes is shared
+        uint8_t* buf8 = reinterpret_cast<uint8_t*>(buf);
+        for (uint32_t i = tid; i < seglen; i += kThreads) {
+            const uint32_t v = pad + i;
+            buf8[lds_dw(v / 4) * 4 + (v & 3u)] = src[i];
+        }
     }
     __syncthreads();
 
-    // Lane's raw CRC over its L bytes (slicing-by-4; leading virtual zeros keep it 0).
-    uint32_t c = 0;
-    const uint32_t* mine = buf + tid * (a.L / 4);
-    for (uint32_t w = 0; w < a.L / 4; ++w) {
-        c ^= mine[w];
-        c = tab[768 + (c & 255u)] ^ tab[512 + ((c >> 8) & 255u)] ^ tab[256 + ((c >> 16) & 255u)] ^ tab[c >> 24];
+    // C independent chains per lane (slicing-by-4; leading virtual zeros keep raw 0).
+    uint32_t c[kChains] = {0u, 0u, 0u, 0u};
+    const uint32_t* mine = buf + tid * kLanePitch;
+#pragma unroll 4
+    for (uint32_t w = 0; w < kChainDw; ++w) {
+#pragma unroll
+        for (int j = 0; j < kChains; ++j) {
+            uint32_t x = c[j] ^ mine[j * kChainDw + w];
+            c[j] = tab[768 + (x & 255u)] ^ tab[512 + ((x >> 8) & 255u)] ^ tab[256 + ((x >> 16) & 255u)] ^ tab[x >> 24];
+        }
     }
+    const cu32 chain = as_const(&a.c->chain[0][0]);
+    uint32_t r = c[3] ^ apply(chain, c[0]);
+    r ^= apply(chain + 32, c[1]);
+    r ^= apply(chain + 64, c[2]);
 
-    // Fold: lanes within a wave (6 levels), then the four waves (2 levels).
+    // Fold lanes: within a wave (6 levels), then the four waves (2 levels).
     const uint32_t lane = tid & 63u;
     const cu32 lvl = as_const(&a.c->lvl[0][0]);
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-        const uint32_t other = __shfl_down(c, 1u << j, 64);
-        if ((lane & ((2u << j) - 1u)) == 0) c = apply(lvl + 32 * j, c) ^ other;
+        const uint32_t other = __shfl_down(r, 1u << j, 64);
+        if ((lane & ((2u << j) - 1u)) == 0) r = apply(lvl + 32 * j, r) ^ other;
     }
-    if (lane == 0) wave_v[tid >> 6] = c;
+    if (lane == 0) wave_v[tid >> 6] = r;
     __syncthreads();
     if (tid == 0) {
         const uint32_t v01 = apply(lvl + 32 * 6, wave_v[0]) ^ wave_v[1];
@@ -187,7 +212,8 @@ Mat32 mat_pow(const Mat32* pow2, uint64_t n) {
     return r;
 }
 
-void build_consts(uint32_t L, uint64_t seg, CrcConsts* c) {
+void build_consts(uint64_t seg, CrcConsts* c) {
+    const uint32_t L = kLaneDw * 4, Lc = kChainDw * 4;
     for (uint32_t i = 0; i < 256; ++i) {
         uint32_t v = i;
         for (int j = 0; j < 8; ++j) v = (v & 1u) ? (v >> 1) ^ kPoly : v >> 1;
@@ -200,6 +226,10 @@ void build_consts(uint32_t L, uint64_t seg, CrcConsts* c) {
     for (int i = 1; i < kPow2; ++i) p[i] = mat_mul(p[i - 1], p[i - 1]);
     for (int i = 0; i < kPow2; ++i)
         for (int j = 0; j < 32; ++j) c->pow2[i][j] = p[i].col[j];
+    for (int j = 0; j < 3; ++j) {
+        const Mat32 m = mat_pow(p, static_cast<uint64_t>(3 - j) * Lc);
+        for (int i = 0; i < 32; ++i) c->chain[j][i] = m.col[i];
+    }
     for (int l = 0; l < 8; ++l) {
         const Mat32 m = mat_pow(p, static_cast<uint64_t>(L) << l);
         for (int j = 0; j < 32; ++j) c->lvl[l][j] = m.col[j];
@@ -209,17 +239,17 @@ void build_consts(uint32_t L, uint64_t seg, CrcConsts* c) {
 }
 
 std::mutex g_mu;
-std::map<std::tuple<int, uint32_t, uint64_t>, CrcConsts*> g_consts;  // device copies, process lifetime
+std::map<std::pair<int, uint64_t>, CrcConsts*> g_consts;  // device copies, process lifetime
 
-hipError_t consts_for(uint32_t L, uint64_t seg, const CrcConsts** out) {
+hipError_t consts_for(uint64_t seg, const CrcConsts** out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> g(g_mu);
-    auto& slot = g_consts[{dev, L, seg}];
+    auto& slot = g_consts[{dev, seg}];
     if (!slot) {
         CrcConsts host;
-        build_consts(L, seg, &host);
+        build_consts(seg, &host);
         CrcConsts* d = nullptr;
         if ((e = hipMalloc(&d, sizeof(CrcConsts))) != hipSuccess) return e;
         if ((e = hipMemcpy(d, &host, sizeof(CrcConsts), hipMemcpyHostToDevice)) != hipSuccess) {
@@ -239,12 +269,9 @@ hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, u
     if (batch == 0 || len == 0) return hipSuccess;
     if (block == 0 || !data || !out) return hipErrorInvalidValue;
     if (block > len) block = len;
-    const uint64_t seg = block < 65536 ? block : 65536;
-    uint32_t L4 = static_cast<uint32_t>((seg + 4 * kThreads - 1) / (4 * kThreads));
-    if ((L4 & 1u) == 0) ++L4;  // odd dword stride per lane: conflict-free LDS reads
-    const uint32_t L = 4 * L4;
+    const uint64_t seg = block < kSegMax ? block : kSegMax;
     const CrcConsts* c = nullptr;
-    hipError_t e = consts_for(L, seg, &c);
+    hipError_t e = consts_for(seg, &c);
     if (e != hipSuccess) return e;
     SegArgs a{};
     a.data = data;
@@ -254,14 +281,13 @@ hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, u
     a.seg = seg;
     a.nblocks = static_cast<uint32_t>((len + block - 1) / block);
     a.segs_per_block = static_cast<uint32_t>((block + seg - 1) / seg);
-    a.L = L;
     a.c = c;
     const uint64_t total_blocks = batch * a.nblocks;
     const uint64_t total_segs = total_blocks * a.segs_per_block;
     if (total_segs > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if ((e = hipMallocAsync(reinterpret_cast<void**>(&a.raw), total_segs * 4, stream)) != hipSuccess) return e;
-    const size_t lds = (1024 + static_cast<size_t>(L4) * kThreads + 4) * 4;
-    hipLaunchKernelGGL(crc_segment_kernel, dim3(static_cast<unsigned>(total_segs)), dim3(kThreads), lds, stream, a);
+    hipLaunchKernelGGL(crc_segment_kernel, dim3(static_cast<unsigned>(total_segs)), dim3(kThreads), kLdsBytes, stream,
+                       a);
     e = hipGetLastError();
     if (e == hipSuccess) {
         hipLaunchKernelGGL(crc_combine_kernel, dim3(static_cast<unsigned>((total_blocks + kThreads - 1) / kThreads)),
