@@ -24,6 +24,7 @@ SIGNATURES = {
     "blbrs_verify": (_I, [_P, _P, _P, ctypes.POINTER(_I)]),
     "blbrs_reconstruct": (_I, [_P, _P, _P]),
     "blbrs_reconstruct_data": (_I, [_P, _P, _P]),
+    "blbrs_reconstruct_verify": (_I, [_P, _P, _P, ctypes.POINTER(_I)]),
     "blbrs_encode_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P]),
     "blbrs_encode_dev_ptrs": (_I, [_P, _P, _SZ, _SZ, _P]),
     "blbrs_reconstruct_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P, _I, _P]),

@@ -458,52 +458,75 @@ bool device_view(const void* p, uint64_t* out) {
     return false;
 }
 
-// Host-memory coding: copy the plan's inputs in, run it, copy its outputs back (or verify).
-// The shard is processed in column chunks alternating over two streams so the H2D of
-// chunk j+1 overlaps the kernel and D2H of chunk j.
-int host_code(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, uint8_t* const* shards,
-              size_t S, Mode mode, int* ok) {
+// One step of a host-memory call: a plan run in store or verify mode.
+struct Step {
+    std::string key;
+    const HostPlan* hp;
+    Mode mode;
+};
+
+// Host-memory coding.  Steps run in order over the same stripe, so a later step sees what
+// an earlier one wrote (Reconstruct then Verify = reconstructAndVerify, store.go:1132-1142,
+// in one device round trip).  Shards read by a step and not produced by an earlier step
+// are copied in once; shards written by store steps are copied out.
+int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const* shards, size_t S, int* ok) {
     WorkerLease lease;
     int rc = lease_worker(lease);
     if (rc) return rc;
     Worker& w = *lease.w;
-    const DevPlan* plan = nullptr;
-    if ((rc = enc->dev_plan(key, hp, w.device, &plan))) return rc;
-
     const int n = enc->k + enc->m;
-    // Zero-copy: when every shard the plan touches is pinned (or device) memory, the kernel
-    // reads and writes it in place over PCIe -- one launch, no staging, and both link
-    // directions busy at once (RS(6,3): 50.8 GiB/s of data vs 37.3 through copy engines;
-    // profiles/r01/zc.txt).
+    std::vector<const DevPlan*> plans(steps.size(), nullptr);
+    std::vector<char> produced(n, 0), need_in(n, 0), is_out(n, 0), touched(n, 0);
+    bool verify = false;
+    for (size_t t = 0; t < steps.size(); ++t) {
+        if ((rc = enc->dev_plan(steps[t].key, *steps[t].hp, w.device, &plans[t]))) return rc;
+        const HostPlan& hp = *steps[t].hp;
+        for (int32_t i : hp.in_idx) {
+            touched[i] = 1;
+            if (!produced[i]) need_in[i] = 1;
+        }
+        for (int32_t i : hp.out_idx) {
+            touched[i] = 1;
+            if (steps[t].mode == Mode::kStore) {
+                produced[i] = 1;
+                is_out[i] = 1;
+            } else {
+                verify = true;
+                if (!produced[i]) need_in[i] = 1;
+            }
+        }
+    }
+    // Zero-copy: when every shard the steps touch is pinned (or device) memory, the kernels
+    // read and write it in place over PCIe -- no staging, and both link directions busy at
+    // once (RS(6,3): 50.8 GiB/s of data vs 37.3 through copy engines; profiles/r01/zc.txt).
     {
         std::vector<uint64_t> view(n, 0);
         bool all = true;
-        for (int32_t i : hp.in_idx) all = all && device_view(shards[i], &view[i]);
-        for (int32_t i : hp.out_idx) all = all && device_view(shards[i], &view[i]);
+        for (int i = 0; i < n && all; ++i)
+            if (touched[i]) all = device_view(shards[i], &view[i]);
         if (all) {
             PtrLease pl;
             Stripes st;
             st.nshards = n;
             if ((rc = upload_table(view.data(), n, w.s[0], pl, &st.ptrs, &st.aligned))) return rc;
-            if (mode == Mode::kVerify) HIP_TRY(hipMemsetAsync(w.dflag, 0, sizeof(int32_t), w.s[0]));
-            if ((rc = run_plan(*plan, st, 1, S, mode, w.dflag, w.s[0]))) return rc;
+            if (verify) HIP_TRY(hipMemsetAsync(w.dflag, 0, sizeof(int32_t), w.s[0]));
+            for (size_t t = 0; t < steps.size(); ++t)
+                if ((rc = run_plan(*plans[t], st, 1, S, steps[t].mode, w.dflag, w.s[0]))) return rc;
             int32_t flag = 0;
-            if (mode == Mode::kVerify)
-                HIP_TRY(hipMemcpyAsync(&flag, w.dflag, sizeof(int32_t), hipMemcpyDeviceToHost, w.s[0]));
+            if (verify) HIP_TRY(hipMemcpyAsync(&flag, w.dflag, sizeof(int32_t), hipMemcpyDeviceToHost, w.s[0]));
             HIP_TRY(hipStreamSynchronize(w.s[0]));
             if (ok) *ok = flag ? 0 : 1;
             return BLBRS_OK;
         }
     }
+    // Staged: 1 MiB column chunks alternate over the worker's two streams, so the H2D of
+    // chunk j+1 overlaps the kernels and D2H of chunk j.
     const size_t Sp = round_up(S, 256);  // padded shard stride keeps every shard 16B-aligned
     if ((rc = w.ensure(static_cast<size_t>(n) * Sp))) return rc;
     const size_t chunk = S <= (size_t{2} << 20) ? S : (size_t{1} << 20);
-    std::vector<bool> is_out(n, false);
-    for (int32_t o : hp.out_idx) is_out[o] = true;
-
-    if (mode == Mode::kVerify) HIP_TRY(hipMemsetAsync(w.dflag, 0, sizeof(int32_t), w.s[0]));
     hipEvent_t ev = nullptr;
-    if (mode == Mode::kVerify) {
+    if (verify) {
+        HIP_TRY(hipMemsetAsync(w.dflag, 0, sizeof(int32_t), w.s[0]));
         HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(ev, w.s[0]));
         HIP_TRY(hipStreamWaitEvent(w.s[1], ev, 0));
@@ -512,11 +535,8 @@ int host_code(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, ui
     for (size_t off = 0; off < S; off += chunk, ++j) {
         const size_t len = std::min(chunk, S - off);
         hipStream_t s = w.s[j & 1];
-        for (int32_t i : hp.in_idx)
-            HIP_TRY(hipMemcpyAsync(w.dbuf + static_cast<size_t>(i) * Sp + off, shards[i] + off, len,
-                                   hipMemcpyHostToDevice, s));
-        if (mode == Mode::kVerify)
-            for (int32_t i : hp.out_idx)
+        for (int i = 0; i < n; ++i)
+            if (need_in[i])
                 HIP_TRY(hipMemcpyAsync(w.dbuf + static_cast<size_t>(i) * Sp + off, shards[i] + off, len,
                                        hipMemcpyHostToDevice, s));
         Stripes st;
@@ -524,14 +544,15 @@ int host_code(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, ui
         st.shard_stride = Sp;
         st.stripe_stride = static_cast<uint64_t>(n) * Sp;
         st.aligned = aligned16(off);
-        if ((rc = run_plan(*plan, st, 1, len, mode, w.dflag, s))) return rc;
-        if (mode == Mode::kStore)
-            for (int32_t i : hp.out_idx)
+        for (size_t t = 0; t < steps.size(); ++t)
+            if ((rc = run_plan(*plans[t], st, 1, len, steps[t].mode, w.dflag, s))) return rc;
+        for (int i = 0; i < n; ++i)
+            if (is_out[i])
                 HIP_TRY(hipMemcpyAsync(shards[i] + off, w.dbuf + static_cast<size_t>(i) * Sp + off, len,
                                        hipMemcpyDeviceToHost, s));
     }
     int32_t flag = 0;
-    if (mode == Mode::kVerify) {
+    if (verify) {
         HIP_TRY(hipEventRecord(ev, w.s[1]));
         HIP_TRY(hipStreamWaitEvent(w.s[0], ev, 0));
         HIP_TRY(hipMemcpyAsync(&flag, w.dflag, sizeof(int32_t), hipMemcpyDeviceToHost, w.s[0]));
@@ -541,6 +562,11 @@ int host_code(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, ui
     if (ev) (void)hipEventDestroy(ev);
     if (ok) *ok = flag ? 0 : 1;
     return BLBRS_OK;
+}
+
+int host_code(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, uint8_t* const* shards,
+              size_t S, Mode mode, int* ok) {
+    return host_run(enc, {Step{key, &hp, mode}}, shards, S, ok);
 }
 
 int current_dev_or_fail(int* dev) { return current_device(dev); }
@@ -611,7 +637,8 @@ int blbrs_verify(blbrs_encoder* enc, const uint8_t* const* shards, const size_t*
     return host_code(enc, "E", *hp, const_cast<uint8_t* const*>(shards), S, Mode::kVerify, ok);
 }
 
-static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens, bool data_only) {
+static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens, bool data_only,
+                            int* verify_ok) {
     if (!enc || !shards || !lens) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     const int n = enc->k + enc->m;
     size_t S = 0;
@@ -623,7 +650,13 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
         present[i] = lens[i] != 0;
         npresent += present[i];
     }
-    if (npresent == n) return BLBRS_OK;
+    auto ep = enc->encode_plan();
+    if (npresent == n) {  // nothing to rebuild; reconstructAndVerify still verifies
+        if (!verify_ok) return BLBRS_OK;
+        for (int i = 0; i < n; ++i)
+            if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
+        return host_code(enc, "E", *ep, shards, S, Mode::kVerify, verify_ok);
+    }
     if (npresent < enc->k) return fail(BLBRS_ERR_TOO_FEW_SHARDS, "too few shards given");
     auto hp = enc->decode_plan(present, data_only, &rc);
     if (!hp) return rc;
@@ -631,19 +664,28 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     for (int32_t i : hp->out_idx)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "missing shard has no output buffer");
-    if (hp->out_idx.empty()) return BLBRS_OK;  // data_only with only parity missing
-    rc = host_code(enc, plan_key(false, present, data_only), *hp, shards, S, Mode::kStore, nullptr);
+    std::vector<Step> steps;
+    if (!hp->out_idx.empty()) steps.push_back(Step{plan_key(false, present, data_only), hp.get(), Mode::kStore});
+    if (verify_ok) steps.push_back(Step{"E", ep.get(), Mode::kVerify});
+    if (steps.empty()) return BLBRS_OK;  // data_only with only parity missing
+    rc = host_run(enc, steps, shards, S, verify_ok);
     if (rc) return rc;
     for (int32_t i : hp->out_idx) lens[i] = S;
     return BLBRS_OK;
 }
 
 int blbrs_reconstruct(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens) {
-    return reconstruct_host(enc, shards, lens, false);
+    return reconstruct_host(enc, shards, lens, false, nullptr);
 }
 
 int blbrs_reconstruct_data(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens) {
-    return reconstruct_host(enc, shards, lens, true);
+    return reconstruct_host(enc, shards, lens, true, nullptr);
+}
+
+int blbrs_reconstruct_verify(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens, int* ok) {
+    if (!ok) return fail(BLBRS_ERR_INVALID_ARG, "ok is NULL");
+    *ok = 0;
+    return reconstruct_host(enc, shards, lens, false, ok);
 }
 
 // ---- device-resident batched path ----

@@ -81,7 +81,7 @@ std::pair<bool, Err> Encoder::Verify(const Shards& shards) {
     return {ok != 0, Err::None};
 }
 
-Err Encoder::reconstruct(Shards& shards, bool data_only) {
+Err Encoder::reconstruct(Shards& shards, bool data_only, bool* verify_ok) {
     const int n = TotalShards();
     if (static_cast<int>(shards.size()) != n) return Err::ErrTooFewShards;
     const size_t size = shard_size(shards);
@@ -102,15 +102,22 @@ Err Encoder::reconstruct(Shards& shards, bool data_only) {
         ptrs[i] = shards[i].data();
         lens[i] = shards[i].len();
     }
-    const int rc = data_only ? blbrs_reconstruct_data(h_, ptrs.data(), lens.data())
-                             : blbrs_reconstruct(h_, ptrs.data(), lens.data());
+    int ok = 0;
+    const int rc = verify_ok ? blbrs_reconstruct_verify(h_, ptrs.data(), lens.data(), &ok)
+                   : data_only ? blbrs_reconstruct_data(h_, ptrs.data(), lens.data())
+                               : blbrs_reconstruct(h_, ptrs.data(), lens.data());
     if (rc != BLBRS_OK) return map_rc(rc);
+    if (verify_ok) *verify_ok = ok != 0;
     for (int i = 0; i < n; ++i)
         if (shards[i].len() == 0 && lens[i] != 0) shards[i] = shards[i].slice(0, size);
     return Err::None;
 }
 
-Err Encoder::Reconstruct(Shards& shards) { return reconstruct(shards, false); }
-Err Encoder::ReconstructData(Shards& shards) { return reconstruct(shards, true); }
+Err Encoder::Reconstruct(Shards& shards) { return reconstruct(shards, false, nullptr); }
+Err Encoder::ReconstructData(Shards& shards) { return reconstruct(shards, true, nullptr); }
+Err Encoder::ReconstructAndVerify(Shards& shards, bool* ok) {
+    *ok = false;
+    return reconstruct(shards, false, ok);
+}
 
 }  // namespace reedsolomon

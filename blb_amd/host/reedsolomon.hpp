@@ -47,6 +47,9 @@ class Encoder {
     std::pair<bool, Err> Verify(const Shards& shards);
     Err Reconstruct(Shards& shards);
     Err ReconstructData(Shards& shards);
+    // Extension: reconstructAndVerify (internal/tractserver/store.go:1132-1142) in one
+    // device round trip.  *ok = false is errVerifyFailed.
+    Err ReconstructAndVerify(Shards& shards, bool* ok);
 
     int DataShards() const { return k_; }
     int ParityShards() const { return m_; }
@@ -57,7 +60,7 @@ class Encoder {
  private:
     friend std::pair<std::unique_ptr<Encoder>, Err> New(int, int);
     Encoder(blbrs_encoder* h, int k, int m) : h_(h), k_(k), m_(m) {}
-    Err reconstruct(Shards& shards, bool data_only);
+    Err reconstruct(Shards& shards, bool data_only, bool* verify_ok);
     blbrs_encoder* h_;
     int k_, m_;
 };

@@ -9,13 +9,9 @@ namespace tractserver {
 
 using core::Error;
 
+// store.go:1132-1142 -- Reconstruct then Verify, fused into one device round trip.
 reedsolomon::Err reconstructAndVerify(reedsolomon::Encoder& enc, reedsolomon::Shards& data, bool* verified) {
-    *verified = false;
-    if (auto e = enc.Reconstruct(data); e != reedsolomon::Err::None) return e;
-    auto [ok, e] = enc.Verify(data);
-    if (e != reedsolomon::Err::None) return e;
-    *verified = ok;
-    return reedsolomon::Err::None;
+    return enc.ReconstructAndVerify(data, verified);
 }
 
 Error Store::RSEncode(core::RSChunkID baseid, int length, const std::vector<core::TSAddr>& srcs,

@@ -193,7 +193,7 @@ class Encoder:
         _check(self._lib.blbrs_verify(self._h, ptrs, L, ctypes.byref(ok)))
         return bool(ok.value)
 
-    def _reconstruct(self, shards: list, data_only: bool, outs: Optional[dict]) -> None:
+    def _reconstruct(self, shards: list, data_only: bool, outs: Optional[dict], verify: bool = False):
         n = self.Shards
         if len(shards) != n:
             raise ErrTooFewShards("too few shards given")
@@ -201,7 +201,7 @@ class Encoder:
         size = self._check_sizes(lens, nilok=True)
         present = [x != 0 for x in lens]
         if all(present):
-            return
+            return self.Verify(shards) if verify else None
         if sum(present) < self.DataShards:
             raise ErrTooFewShards("too few shards given")
         kind = self._kind(shards)
@@ -227,14 +227,23 @@ class Encoder:
             ref = next(s for s in shards if _shard_len(s))
             _check(self._lib.blbrs_reconstruct_dev_ptrs(self._h, ptrs, 1, size, pres, int(data_only),
                                                          _torch_stream(ref)))
+            for i in produce:
+                shards[i] = bufs[i]
+            return self.Verify(shards) if verify else None
+        ptrs = (ctypes.c_void_p * n)(*[_host_ptr(bufs[i]) if (present[i] or i in produce) else None
+                                       for i in range(n)])
+        L = (ctypes.c_size_t * n)(*lens)
+        ok = None
+        if verify:
+            okc = ctypes.c_int(0)
+            _check(self._lib.blbrs_reconstruct_verify(self._h, ptrs, L, ctypes.byref(okc)))
+            ok = bool(okc.value)
         else:
-            ptrs = (ctypes.c_void_p * n)(*[_host_ptr(bufs[i]) if (present[i] or i in produce) else None
-                                           for i in range(n)])
-            L = (ctypes.c_size_t * n)(*lens)
             fn = self._lib.blbrs_reconstruct_data if data_only else self._lib.blbrs_reconstruct
             _check(fn(self._h, ptrs, L))
         for i in produce:
             shards[i] = bufs[i]
+        return ok
 
     def Reconstruct(self, shards: list, outs: Optional[dict] = None) -> None:
         """Rebuild every missing shard (data and parity) in the list."""
@@ -243,6 +252,11 @@ class Encoder:
     def ReconstructData(self, shards: list, outs: Optional[dict] = None) -> None:
         """Rebuild missing data shards only; parity slots stay missing."""
         self._reconstruct(shards, True, outs)
+
+    def ReconstructAndVerify(self, shards: list, outs: Optional[dict] = None) -> bool:
+        """reconstructAndVerify (internal/tractserver/store.go:1132-1142): Reconstruct, then
+        Verify the completed stripe -- for host shards in one device round trip."""
+        return bool(self._reconstruct(shards, False, outs, verify=True))
 
     # ---- batched device-resident path ----
     def _stripes(self, stripes):

@@ -78,9 +78,9 @@ class _VerifyFailed(Exception):
 
 
 def reconstruct_and_verify(enc: reedsolomon.Encoder, data: list) -> None:
-    """store.go:1132-1142: Reconstruct, then Verify (full parity recompute + compare)."""
-    enc.Reconstruct(data)
-    if not enc.Verify(data):
+    """store.go:1132-1142: Reconstruct, then Verify (full parity recompute + compare); both
+    run in one device round trip (blbrs_reconstruct_verify)."""
+    if not enc.ReconstructAndVerify(data):
         raise _VerifyFailed("verification failed")
 
 

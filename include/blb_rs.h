@@ -82,6 +82,11 @@ int blbrs_reconstruct(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens);
 /* Encoder.ReconstructData: rebuild missing data shards only; parity slots untouched. */
 int blbrs_reconstruct_data(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens);
 
+/* reconstructAndVerify (internal/tractserver/store.go:1132-1142) in one device round trip:
+ * Reconstruct, then Verify the completed stripe while it is still on the GPU.  Same
+ * arguments and errors as blbrs_reconstruct; *ok = 0 is store.go's errVerifyFailed. */
+int blbrs_reconstruct_verify(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens, int* ok);
+
 /* ---- device-resident batched path (stripes already in HBM) ----
  * Strided layout: shard i of stripe b lives at
  *     stripes + b * stripe_stride + i * shard_stride          (i in [0, k+m))

@@ -417,3 +417,23 @@ def test_streaming_host_batch_pageable_fallback(oracle_lib):
         want = oracle_encode(oracle_lib, k, m, st[:k])
         for j in range(m):
             assert np.array_equal(st[k + j], want[j])
+
+
+def test_reconstruct_and_verify_fused(oracle_lib):
+    """reconstructAndVerify (store.go:1132-1142) in one round trip: true for a consistent
+    stripe (incl. when nothing is missing), false when a surviving shard disagrees."""
+    for k, m, S in [(3, 2, 20000), (6, 3, (1 << 20) + 5), (10, 4, 4096)]:
+        rng = np.random.default_rng(S)
+        enc = rs.New(k, m)
+        full = rand_shards(rng, k, S) + [np.empty(S, np.uint8) for _ in range(m)]
+        enc.Encode(full)
+        cur = [None if i in (1, k) else full[i].copy() for i in range(k + m)]
+        assert enc.ReconstructAndVerify(cur)
+        assert all(np.array_equal(a, b) for a, b in zip(cur, full))
+        assert enc.ReconstructAndVerify([s.copy() for s in full])
+        bad = [None if i == 1 else full[i].copy() for i in range(k + m)]
+        bad[k + m - 1][S // 2] ^= 0x5A   # an extra present parity that disagrees
+        assert not enc.ReconstructAndVerify(bad)
+        pinned = [None if i == 0 else torch.from_numpy(full[i].copy()).pin_memory().numpy() for i in range(k + m)]
+        assert enc.ReconstructAndVerify(pinned)   # zero-copy variant
+        assert np.array_equal(pinned[0], full[0])
