@@ -81,3 +81,27 @@ def test_gpu_crc32c_batch_of_parity_shards(oracle_lib):
     for r in range(B * m):
         assert np.array_equal(crc_blocks[r], oracle_lib.crc32c_blocks(host[r], 65532)), r
         assert int(crc_whole[r, 0]) == oracle_lib.crc32c(host[r]), r
+
+
+@gpu
+def test_gpu_crc32c_aligned_shapes(oracle_lib):
+    """Dword-aligned lengths/blocks/strides take the streaming kernel: sweep the virtual
+    zero-prefix cases (none, inside row 0, several whole rows) and strided batches."""
+    from blb_amd import checksum
+    torch = _torch()
+    rng = np.random.default_rng(11)
+    cases = [(65532, 4 * 65532), (65536, 65536 * 3), (4096, 4096 * 5 + 8), (4, 64), (8, 4100),
+             (60000, 180004), (4100, 65536 + 4), (0, 4), (0, 4092), (0, 4096 + 4), (0, 65532),
+             (0, 65536 + 65532), (131072, 131072 + 12)]
+    for _ in range(12):
+        blk = int(rng.integers(1, 40000)) * 4
+        cases.append((blk, int(rng.integers(1, 80000)) * 4))
+    for blk, n in cases:
+        batch = int(rng.integers(1, 4))
+        stride = n + 4 * int(rng.integers(0, 40))
+        host = rng.integers(0, 256, (batch, stride), dtype=np.uint8)
+        dev = torch.from_numpy(host).cuda()
+        got = checksum.as_uint32(checksum.ChecksumBatch(dev[:, :n], blk))
+        for r in range(batch):
+            want = oracle_lib.crc32c_blocks(host[r, :n], blk or n)
+            assert np.array_equal(got[r], want), (blk, n, r)
