@@ -199,6 +199,44 @@ def main():
         crc_ms = crc_evs[0].elapsed_time(crc_evs[1])
         extra["crc32c_parity_blocks"] = {"GBps": round(B * m * S / (crc_ms * 1e-3) / 1e9, 1),
                                          "ms": round(crc_ms, 3), "bytes": B * m * S, "block": 65532}
+        # PackTracts (§8f row 3): lay tracts of random length (64 KiB..8 MiB, from a 4 GiB
+        # device pool) at padToLength-aligned offsets into the B*k data pieces, zero-filling
+        # holes and tails.  HBM bytes = tract bytes read + piece bytes written.
+        from blb_amd import pack
+        pool = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev)
+        prng = np.random.default_rng(17)
+        per_col = []
+        read_bytes = 0
+        for j in range(k):
+            ext = []
+            for b in range(B):
+                off = 0
+                while True:
+                    ln = int(prng.integers(64 << 10, (8 << 20) + 1))
+                    if off + ln > S:
+                        break
+                    src = int(prng.integers(0, pool.numel() - ln))
+                    ext.append((pool[src:], off, ln, b))
+                    read_bytes += ln
+                    off += pack.padded_length(ln)
+            per_col.append(ext)
+        cols = [stripes[:, j, :] for j in range(k)]
+        for j in range(k):
+            pack.PackPieces(cols[j], S, per_col[j])
+        torch.cuda.synchronize(dev)
+        pk_evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.cuda._sleep(400_000_000)  # keeps the host-side extent checks outside the window
+        pk_evs[0].record(stream)
+        for j in range(k):
+            pack.PackPieces(cols[j], S, per_col[j])
+        pk_evs[1].record(stream)
+        torch.cuda.synchronize(dev)
+        pk_ms = pk_evs[0].elapsed_time(pk_evs[1])
+        pk_bytes = read_bytes + B * k * S
+        extra["pack_tracts"] = {"hbm_GBps": round(pk_bytes / (pk_ms * 1e-3) / 1e9, 1), "ms": round(pk_ms, 3),
+                                "pieces": B * k, "tracts": sum(len(e) for e in per_col),
+                                "bytes_read": read_bytes, "bytes_written": B * k * S}
+        del pool, per_col
         # BASELINE config 5 shape on one GPU: PCIe-inclusive streaming from pinned host.
         nb = 16
         pinned = torch.empty((nb, k + m, S), dtype=torch.uint8).pin_memory()

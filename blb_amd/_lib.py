@@ -34,6 +34,7 @@ SIGNATURES = {
     "blbrs_encode_host_batch": (_I, [_P, _P, _SZ, _SZ, _I]),
     "blbrs_crc32c_dev": (_I, [_P, _SZ, _SZ, _SZ, _SZ, _P, _P]),
     "blbrs_crc32c": (_I, [_P, _SZ, _SZ, _P]),
+    "blbrs_pack_dev": (_I, [_P, _SZ, _SZ, _SZ, _P, _SZ, _P]),
     "blbrs_set_device": (_I, [_I]),
     "blbrs_device_count": (_I, [ctypes.POINTER(_I)]),
     "blbrs_last_error": (ctypes.c_char_p, []),

@@ -28,6 +28,7 @@ class Error(enum.Enum):
     ErrRPC = "rpc error"
     ErrUnknown = "unknown error"
     ErrAllocHost = "could not allocate host"
+    ErrNoSuchTract = "tract does not exist"
 
 
 class StorageClass(enum.IntEnum):
@@ -51,6 +52,22 @@ def rs_params(cls: StorageClass) -> tuple[int, int]:
 class TractID:
     blob: int
     index: int
+
+    def is_valid(self) -> bool:
+        """internal/core/ids.go:237-239: a valid regular blob, or any RS-partition blob."""
+        p = (self.blob >> 32) & 0xFFFFFFFF
+        regular = (p & 0x3FFFFFFF) != 0 and (p >> 30) == 0 and (self.blob & 0xFFFFFFFF) > 0
+        return regular or ((p & 0x3FFFFFFF) != 0 and (p >> 30) == 2)
+
+
+def blob_id_from_parts(partition: int, key: int) -> int:
+    """internal/core/ids.go:196-198 BlobIDFromParts."""
+    return ((partition & 0xFFFFFFFF) << 32) | (key & 0xFFFFFFFF)
+
+
+def tract_id_from_parts(blob: int, index: int) -> TractID:
+    """internal/core/ids.go:242-244 TractIDFromParts."""
+    return TractID(blob, index)
 
 
 @dataclass(frozen=True)

@@ -26,6 +26,7 @@
 
 #include "../../include/blb_rs.h"
 #include "crc32c.hpp"
+#include "pack.hpp"
 #include "gf256.hpp"
 #include "rs_kernels.hpp"
 
@@ -936,6 +937,67 @@ int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {
     (void)hipFreeAsync(dout, w.s[0]);
     if (e == hipSuccess) e = hipStreamSynchronize(w.s[0]);
     if (e != hipSuccess) return hip_fail(e, "crc32c");
+    return BLBRS_OK;
+}
+
+// ---- PackTracts ----
+
+int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece_len,
+                   const blbrs_pack_extent* extents, size_t nextents, void* stream) {
+    if (npieces == 0 || piece_len == 0) {
+        if (nextents) return fail(BLBRS_ERR_INVALID_ARG, "extents given for empty pieces");
+        return BLBRS_OK;
+    }
+    if (!dst || (nextents && !extents)) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (npieces > 1 && dst_stride < piece_len) return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than piece length");
+    int dev = 0;
+    int rc = current_dev_or_fail(&dev);
+    if (rc) return rc;
+    uint64_t dview = 0;
+    if (!device_view(dst, &dview)) return fail(BLBRS_ERR_INVALID_ARG, "pack destination is not device-accessible");
+    // checkTractSpec (store.go:996-1009) per piece, plus the table: piece starts, then
+    // {src, offset, length, piece} per extent.
+    std::vector<uint64_t> table(npieces + 1 + 4 * nextents);
+    uint64_t* ex = table.data() + npieces + 1;
+    size_t next_piece = 0;
+    uint64_t end = 0;
+    const uint8_t* last_src = nullptr;
+    uint64_t last_view = 0;
+    for (size_t i = 0; i < nextents; ++i) {
+        const blbrs_pack_extent& x = extents[i];
+        if (x.piece >= npieces || x.piece + 1 < next_piece)
+            return fail(BLBRS_ERR_INVALID_ARG, "extent " + std::to_string(i) + ": piece out of range or out of order");
+        while (next_piece <= x.piece) {
+            table[next_piece++] = i;
+            end = 0;
+        }
+        if (x.offset < end || x.length > piece_len || x.offset > piece_len - x.length)
+            return fail(BLBRS_ERR_INVALID_ARG, "extent " + std::to_string(i) + " overlaps, is out of order or exceeds the piece");
+        end = x.offset + x.length;
+        uint64_t sview = 0;
+        if (x.length) {
+            if (!x.src) return fail(BLBRS_ERR_INVALID_ARG, "extent " + std::to_string(i) + ": NULL source");
+            if (x.src == last_src) {
+                sview = last_view;
+            } else if (!device_view(x.src, &sview)) {
+                return fail(BLBRS_ERR_INVALID_ARG, "extent " + std::to_string(i) + ": source is not device-accessible");
+            }
+            last_src = x.src;
+            last_view = sview;
+        }
+        ex[4 * i] = sview;
+        ex[4 * i + 1] = x.offset;
+        ex[4 * i + 2] = x.length;
+        ex[4 * i + 3] = x.piece;
+    }
+    while (next_piece <= npieces) table[next_piece++] = nextents;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    PtrLease lease;
+    const uint64_t* tdev = nullptr;
+    bool unused = false;
+    if ((rc = upload_table(table.data(), table.size(), s, lease, &tdev, &unused))) return rc;
+    hipError_t e = pack_pieces(reinterpret_cast<uint8_t*>(dview), dst_stride, npieces, piece_len, tdev, s);
+    if (e != hipSuccess) return hip_fail(e, "pack_pieces");
     return BLBRS_OK;
 }
 

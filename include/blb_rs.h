@@ -138,6 +138,26 @@ int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t le
 /* Host-memory form: one buffer; out (host) has ceil(len / block) entries. */
 int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out);
 
+/* ---- PackTracts: device assembly of packed RS data pieces ----
+ * The byte work of Store.PackTracts (internal/tractserver/store.go:922-994), for `npieces`
+ * pieces at once.  Piece p is dst + p * dst_stride, piece_len bytes (the PackTracts
+ * `length`).  It receives every extent with .piece == p at .offset (t.write(b, src.Offset),
+ * store.go:957), and ZERO in every byte no extent covers: the holes before and between
+ * tracts (sparse-file reads) and the pad up to piece_len (store.go:974-980).  Extents must
+ * be sorted by (piece, offset), non-overlapping and end inside piece_len, which is
+ * checkTractSpec (store.go:996-1009); anything else is BLBRS_ERR_INVALID_ARG.  dst and
+ * every source must be device-accessible: device memory or pinned host memory
+ * (hipHostMalloc / hipHostRegister), read in place over PCIe.  Asynchronous on `stream`;
+ * the extent array may be reused as soon as the call returns. */
+typedef struct {
+    const uint8_t* src; /* the tract bytes (CtlRead reply) */
+    uint64_t offset;    /* PackTractSpec.Offset */
+    uint64_t length;    /* PackTractSpec.Length */
+    uint64_t piece;     /* destination piece index */
+} blbrs_pack_extent;
+int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece_len,
+                   const blbrs_pack_extent* extents, size_t nextents, void* stream);
+
 /* ---- misc ---- */
 int blbrs_set_device(int device);      /* hipSetDevice for the calling thread */
 int blbrs_device_count(int* count);

@@ -180,3 +180,16 @@ def crc32c(data: bytes, crc: int = 0) -> int:
         for _ in range(8):
             crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
     return ~crc & 0xFFFFFFFF
+
+
+def pack_piece(length: int, srcs: list[tuple[bytes, int]]) -> bytes:
+    """The packed chunk file Store.PackTracts leaves (internal/tractserver/store.go:922-994):
+    each (tract bytes, Offset) written at its offset (t.write, :957), zero holes (a fresh
+    sparse file reads 0), then zeros up to `length` when there are sources (:974-980).
+    With no sources the file stays empty."""
+    if not srcs:
+        return b""
+    out = bytearray(max(length, max(off + len(b) for b, off in srcs)))
+    for b, off in srcs:
+        out[off:off + len(b)] = b
+    return bytes(out)
