@@ -35,6 +35,10 @@ SIGNATURES = {
     "blbrs_crc32c_dev": (_I, [_P, _SZ, _SZ, _SZ, _SZ, _P, _P]),
     "blbrs_crc32c": (_I, [_P, _SZ, _SZ, _P]),
     "blbrs_pack_dev": (_I, [_P, _SZ, _SZ, _SZ, _P, _SZ, _P]),
+    "blbrs_batcher_new": (_I, [_I, _I, ctypes.POINTER(_P)]),
+    "blbrs_batcher_free": (None, [_P]),
+    "blbrs_encoder_set_batcher": (_I, [_P, _P]),
+    "blbrs_batcher_stats": (_I, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "blbrs_set_device": (_I, [_I]),
     "blbrs_device_count": (_I, [ctypes.POINTER(_I)]),
     "blbrs_last_error": (ctypes.c_char_p, []),

@@ -16,12 +16,17 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/blb_rs.h"
@@ -143,7 +148,11 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
 // Encoder
 // ---------------------------------------------------------------------------------------
 
-struct blbrs_encoder {
+// Matrix and plan caches of one (k, m).  Shared by every blbrs_encoder handle with that
+// shape: blb makes a fresh reedsolomon.New(n, m) per client reconstruct
+// (client/blb/reconstruct.go:172), and a shared core keeps those calls from rebuilding
+// and re-uploading plans -- and lets a batcher merge them.
+struct EncoderCore {
     int k = 0, m = 0;
     Mat matrix;  // (k+m) x k systematic encoding matrix
     std::mutex mu;
@@ -227,7 +236,36 @@ struct blbrs_encoder {
     }
 };
 
+struct blbrs_encoder {
+    std::shared_ptr<EncoderCore> core;
+    int k = 0, m = 0;
+    std::atomic<blbrs_batcher*> batcher{nullptr};  // routes host Reconstruct[Data] (blbrs_encoder_set_batcher)
+    std::shared_ptr<HostPlan> encode_plan() { return core->encode_plan(); }
+    std::shared_ptr<HostPlan> decode_plan(const std::vector<uint8_t>& present, bool data_only, int* rc) {
+        return core->decode_plan(present, data_only, rc);
+    }
+    int dev_plan(const std::string& key, const HostPlan& hp, int device, const DevPlan** out) {
+        return core->dev_plan(key, hp, device, out);
+    }
+};
+
 namespace {
+
+std::mutex g_cores_mu;
+std::map<std::pair<int, int>, std::weak_ptr<EncoderCore>> g_cores;
+
+// The shared core for (k, m); nullptr when the matrix cannot be built.
+std::shared_ptr<EncoderCore> core_for(int k, int m) {
+    std::lock_guard<std::mutex> g(g_cores_mu);
+    auto& w = g_cores[{k, m}];
+    if (auto c = w.lock()) return c;
+    auto c = std::make_shared<EncoderCore>();
+    c->k = k;
+    c->m = m;
+    if (!build_matrix(k, m, c->matrix)) return nullptr;
+    w = c;
+    return c;
+}
 
 std::string plan_key(bool encode, const std::vector<uint8_t>& present, bool data_only) {
     if (encode) return "E";
@@ -578,6 +616,161 @@ std::vector<uint8_t> present_vec(const blbrs_encoder* enc, const uint8_t* presen
     return p;
 }
 
+// ---- batched host reconstructs ----
+//
+// client/blb/reconstruct.go:65-195 calls ReconstructData once per degraded read, on one
+// stripe of `length`-byte pieces; MaxInFlight (:19,35-45) lets many run at once.  Alone,
+// each call is a launch plus a stream round trip for a few KiB..MiB of work.  A batcher
+// collects the calls that arrive within `window_us` (or until `max_batch` are waiting) and
+// runs them as ONE launch per (encoder, erasure pattern, length) group over a device
+// pointer table, with one stream sync for the whole batch.  Shards in pinned or device
+// memory are used in place; pageable shards are staged by the CALLING thread through its
+// own pinned buffer, so the memcpys of concurrent callers run in parallel.
+struct BatchReq {
+    blbrs_encoder* enc = nullptr;
+    std::shared_ptr<HostPlan> hp;
+    std::string key;
+    std::vector<uint64_t> views;  // device-visible address per shard slot (0 = unused)
+    size_t S = 0;
+    std::chrono::steady_clock::time_point arrival;
+    int rc = BLBRS_OK;
+    bool done = false;
+};
+
+// Per-thread pinned staging for pageable shards.
+struct PinnedStage {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    ~PinnedStage() {
+        if (p) (void)hipHostFree(p);
+    }
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return BLBRS_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p), bytes, hipHostMallocDefault));
+        cap = bytes;
+        return BLBRS_OK;
+    }
+};
+
+}  // namespace
+
+struct blbrs_batcher {
+    int device = 0;
+    size_t max_batch = 64;
+    std::chrono::microseconds window{200};
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::condition_variable cv_in, cv_done;
+    std::deque<BatchReq*> q;
+    bool stop = false;
+    std::thread th;
+    std::atomic<uint64_t> launches{0}, requests{0};
+
+    void run() {
+        (void)hipSetDevice(device);
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv_in.wait(lk, [&] { return stop || !q.empty(); });
+            if (q.empty()) return;  // stop requested and nothing left
+            const auto deadline = q.front()->arrival + window;
+            cv_in.wait_until(lk, deadline, [&] { return stop || q.size() >= max_batch; });
+            std::vector<BatchReq*> batch;
+            while (!q.empty() && batch.size() < max_batch) {
+                batch.push_back(q.front());
+                q.pop_front();
+            }
+            lk.unlock();
+            process(batch);
+            lk.lock();
+            for (BatchReq* r : batch) r->done = true;
+            cv_done.notify_all();
+        }
+    }
+
+    void process(std::vector<BatchReq*>& batch) {
+        // Handles of one (k, m) share a core, so calls from different encoders merge.
+        std::map<std::tuple<EncoderCore*, std::string, size_t>, std::vector<BatchReq*>> groups;
+        for (BatchReq* r : batch) groups[{r->enc->core.get(), r->key, r->S}].push_back(r);
+        for (auto& [gk, reqs] : groups) {
+            EncoderCore* enc = std::get<0>(gk);
+            const size_t S = std::get<2>(gk), n = static_cast<size_t>(enc->k + enc->m);
+            const DevPlan* plan = nullptr;
+            int rc = enc->dev_plan(std::get<1>(gk), *reqs[0]->hp, device, &plan);
+            if (rc == BLBRS_OK) {
+                std::vector<uint64_t> table(reqs.size() * n);
+                for (size_t j = 0; j < reqs.size(); ++j)
+                    std::copy(reqs[j]->views.begin(), reqs[j]->views.end(), table.begin() + j * n);
+                PtrLease pl;
+                Stripes st;
+                st.nshards = static_cast<uint32_t>(n);
+                rc = upload_table(table.data(), table.size(), stream, pl, &st.ptrs, &st.aligned);
+                if (rc == BLBRS_OK) rc = run_plan(*plan, st, reqs.size(), S, Mode::kStore, nullptr, stream);
+                if (rc == BLBRS_OK) launches.fetch_add(1);
+            }
+            for (BatchReq* r : reqs) r->rc = rc;
+        }
+        const hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) {
+            const int rc = hip_fail(e, "batched reconstruct");
+            for (BatchReq* r : batch) r->rc = rc;
+        }
+        requests.fetch_add(batch.size());
+    }
+};
+
+namespace {
+
+// The host Reconstruct / ReconstructData of one stripe through `b` (blocking).  `hp` is
+// the decode plan with at least one output; argument checks have been done.
+int batched_reconstruct(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key,
+                        std::shared_ptr<HostPlan> hp, uint8_t* const* shards, size_t S) {
+    static thread_local PinnedStage stage;
+    const int n = enc->k + enc->m;
+    BatchReq req;
+    req.enc = enc;
+    req.hp = hp;
+    req.key = key;
+    req.S = S;
+    req.views.assign(n, 0);
+    // Slots touched by the plan: inputs then outputs; pageable ones get a staging slot.
+    std::vector<std::pair<int, bool>> touched;
+    for (int32_t i : hp->in_idx) touched.push_back({i, true});
+    for (int32_t i : hp->out_idx) touched.push_back({i, false});
+    const size_t Sp = round_up(S, 256);
+    size_t nstaged = 0;
+    std::vector<int> slot(n, -1);
+    for (auto [i, in] : touched) {
+        (void)in;
+        if (!device_view(shards[i], &req.views[i])) slot[i] = static_cast<int>(nstaged++);
+    }
+    if (nstaged) {
+        int rc = stage.ensure(nstaged * Sp);
+        if (rc) return rc;
+        for (auto [i, in] : touched) {
+            if (slot[i] < 0) continue;
+            uint8_t* p = stage.p + static_cast<size_t>(slot[i]) * Sp;
+            if (in) std::memcpy(p, shards[i], S);
+            if (!device_view(p, &req.views[i])) return fail(BLBRS_ERR_HIP, "pinned staging has no device mapping");
+        }
+    }
+    req.arrival = std::chrono::steady_clock::now();
+    {
+        std::unique_lock<std::mutex> lk(b->mu);
+        if (b->stop) return fail(BLBRS_ERR_INVALID_ARG, "batcher is shutting down");
+        b->q.push_back(&req);
+        if (b->q.size() >= b->max_batch) b->cv_in.notify_one();
+        else if (b->q.size() == 1) b->cv_in.notify_one();
+        b->cv_done.wait(lk, [&] { return req.done; });
+    }
+    if (req.rc != BLBRS_OK) return req.rc;
+    for (int32_t i : hp->out_idx)
+        if (slot[i] >= 0) std::memcpy(shards[i], stage.p + static_cast<size_t>(slot[i]) * Sp, S);
+    return BLBRS_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
@@ -592,13 +785,12 @@ int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out) {
         return fail(BLBRS_ERR_INV_SHARD_NUM, "cannot create Encoder with zero or less data/parity shards");
     if (data_shards + parity_shards > 256)
         return fail(BLBRS_ERR_MAX_SHARD_NUM, "cannot create Encoder with more than 256 data+parity shards");
+    auto core = core_for(data_shards, parity_shards);
+    if (!core) return fail(BLBRS_ERR_SINGULAR, "matrix is singular");
     auto* e = new blbrs_encoder();
+    e->core = std::move(core);
     e->k = data_shards;
     e->m = parity_shards;
-    if (!build_matrix(data_shards, parity_shards, e->matrix)) {
-        delete e;
-        return fail(BLBRS_ERR_SINGULAR, "matrix is singular");
-    }
     *out = e;
     return BLBRS_OK;
 }
@@ -609,8 +801,9 @@ int blbrs_parity_shards(const blbrs_encoder* enc) { return enc ? enc->m : 0; }
 
 int blbrs_matrix(const blbrs_encoder* enc, uint8_t* out, size_t cap) {
     if (!enc || !out) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
-    if (cap < enc->matrix.size()) return fail(BLBRS_ERR_INVALID_ARG, "buffer too small");
-    std::memcpy(out, enc->matrix.data(), enc->matrix.size());
+    const Mat& mat = enc->core->matrix;
+    if (cap < mat.size()) return fail(BLBRS_ERR_INVALID_ARG, "buffer too small");
+    std::memcpy(out, mat.data(), mat.size());
     return BLBRS_OK;
 }
 
@@ -665,6 +858,12 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     for (int32_t i : hp->out_idx)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "missing shard has no output buffer");
+    blbrs_batcher* b = verify_ok ? nullptr : enc->batcher.load();
+    if (b && !hp->out_idx.empty()) {
+        if ((rc = batched_reconstruct(b, enc, plan_key(false, present, data_only), hp, shards, S))) return rc;
+        for (int32_t i : hp->out_idx) lens[i] = S;
+        return BLBRS_OK;
+    }
     std::vector<Step> steps;
     if (!hp->out_idx.empty()) steps.push_back(Step{plan_key(false, present, data_only), hp.get(), Mode::kStore});
     if (verify_ok) steps.push_back(Step{"E", ep.get(), Mode::kVerify});
@@ -937,6 +1136,54 @@ int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {
     (void)hipFreeAsync(dout, w.s[0]);
     if (e == hipSuccess) e = hipStreamSynchronize(w.s[0]);
     if (e != hipSuccess) return hip_fail(e, "crc32c");
+    return BLBRS_OK;
+}
+
+// ---- batched client reconstructs ----
+
+int blbrs_batcher_new(int max_batch, int window_us, blbrs_batcher** out) {
+    if (!out) return fail(BLBRS_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    if (max_batch <= 0 || window_us < 0) return fail(BLBRS_ERR_INVALID_ARG, "max_batch must be > 0, window_us >= 0");
+    int dev = 0;
+    int rc = current_dev_or_fail(&dev);
+    if (rc) return rc;
+    auto* b = new blbrs_batcher();
+    b->device = dev;
+    b->max_batch = static_cast<size_t>(max_batch);
+    b->window = std::chrono::microseconds(window_us);
+    hipError_t e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete b;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    b->th = std::thread([b] { b->run(); });
+    *out = b;
+    return BLBRS_OK;
+}
+
+void blbrs_batcher_free(blbrs_batcher* b) {
+    if (!b) return;
+    {
+        std::lock_guard<std::mutex> g(b->mu);
+        b->stop = true;
+    }
+    b->cv_in.notify_all();
+    b->th.join();  // drains the queue first
+    (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+int blbrs_batcher_stats(const blbrs_batcher* b, uint64_t* requests, uint64_t* launches) {
+    if (!b || !requests || !launches) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    *requests = b->requests.load();
+    *launches = b->launches.load();
+    return BLBRS_OK;
+}
+
+int blbrs_encoder_set_batcher(blbrs_encoder* enc, blbrs_batcher* b) {
+    if (!enc) return fail(BLBRS_ERR_INVALID_ARG, "enc is NULL");
+    enc->batcher.store(b);
     return BLBRS_OK;
 }
 

@@ -128,6 +128,12 @@ class Encoder:
             self._lib.blbrs_free(h)
             self._h = None
 
+    def SetBatcher(self, batcher: Optional["Batcher"]) -> None:
+        """Route this encoder's host Reconstruct / ReconstructData calls through `batcher`
+        (None detaches).  Results and errors are unchanged; concurrent callers share launches."""
+        _check(self._lib.blbrs_encoder_set_batcher(self._h, batcher._h if batcher else None))
+        self._batcher = batcher  # keep it alive while attached
+
     # ---- introspection ----
     def matrix(self) -> np.ndarray:
         out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
@@ -313,6 +319,35 @@ class Encoder:
                 flat.append(_host_ptr(s))
         ptrs = (ctypes.c_void_p * len(flat))(*flat)
         _check(self._lib.blbrs_encode_host_batch(self._h, ptrs, B, S, int(nstreams)))
+
+
+class Batcher:
+    """Batching queue for concurrent host Reconstruct / ReconstructData calls (SURVEY.md §8f
+    row 4; client/blb/reconstruct.go:65-195 with MaxInFlight > 1).  Calls that arrive
+    within `window_us` of the first waiting one (or until `max_batch` wait) run as one
+    kernel launch per (shape, erasure pattern, length) group.  Attach with
+    Encoder.SetBatcher; free only after detaching from every encoder."""
+
+    def __init__(self, max_batch: int = 64, window_us: int = 200):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        _check(self._lib.blbrs_batcher_new(int(max_batch), int(window_us), ctypes.byref(h)))
+        self._h = h
+
+    def stats(self) -> tuple[int, int]:
+        """(calls served, kernel launches issued)."""
+        r, l = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._lib.blbrs_batcher_stats(self._h, ctypes.byref(r), ctypes.byref(l)))
+        return int(r.value), int(l.value)
+
+    def close(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.blbrs_batcher_free(h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 def New(data_shards: int, parity_shards: int) -> Encoder:

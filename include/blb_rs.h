@@ -51,6 +51,7 @@ extern "C" {
 #define BLBRS_ERR_NO_DEVICE     (-9) /* no gfx950 device visible */
 
 typedef struct blbrs_encoder blbrs_encoder;
+typedef struct blbrs_batcher blbrs_batcher;
 
 /* ---- construction (reedsolomon.New) ---- */
 
@@ -137,6 +138,24 @@ int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t le
                      uint32_t* out_dev, void* stream);
 /* Host-memory form: one buffer; out (host) has ceil(len / block) entries. */
 int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out);
+
+/* ---- batched client reconstructs ----
+ * client/blb/reconstruct.go:65-195 calls ReconstructData once per degraded read (one stripe
+ * of `length`-byte pieces), up to MaxInFlight (:19,35-45) at once.  A batcher collects
+ * concurrent host Reconstruct / ReconstructData calls that arrive within window_us (or
+ * until max_batch wait) and runs them as one kernel launch per (encoder, erasure pattern,
+ * length) group plus one stream sync.  Attach it to an encoder and the plain
+ * blbrs_reconstruct / blbrs_reconstruct_data calls on that encoder go through it: same
+ * arguments, results and errors, the caller still blocks until its own stripe is done --
+ * the Go Encoder interface is unchanged.  (blbrs_reconstruct_verify is never batched.)
+ * Pinned / device shards are used in place; pageable ones are staged by the calling thread.
+ * The batcher runs on the device current at creation; free it after detaching it from
+ * every encoder. */
+int blbrs_batcher_new(int max_batch, int window_us, blbrs_batcher** out);
+void blbrs_batcher_free(blbrs_batcher* b);
+int blbrs_encoder_set_batcher(blbrs_encoder* enc, blbrs_batcher* b); /* b = NULL detaches */
+/* Counters: calls served and kernel launches issued so far. */
+int blbrs_batcher_stats(const blbrs_batcher* b, uint64_t* requests, uint64_t* launches);
 
 /* ---- PackTracts: device assembly of packed RS data pieces ----
  * The byte work of Store.PackTracts (internal/tractserver/store.go:922-994), for `npieces`
