@@ -29,10 +29,51 @@ import (
 	"errors"
 	"io"
 	"runtime"
+	"sync/atomic"
 	"unsafe"
 
 	"github.com/klauspost/reedsolomon"
 )
+
+// batcher, when set by EnableBatching, is attached to every encoder New returns.
+var batcher atomic.Pointer[C.blbrs_batcher]
+
+// EnableBatching makes every encoder created afterwards route its Reconstruct /
+// ReconstructData calls through one process-wide batcher (blb_rs.h: blbrs_batcher_new):
+// concurrent degraded reads (client/blb/reconstruct.go with ReconstructBehavior.MaxInFlight
+// > 1) then share kernel launches.  Call once at client start-up, before reads begin.
+func EnableBatching(maxBatch, windowMicros int) error {
+	var b *C.blbrs_batcher
+	if rc := C.blbrs_batcher_new(C.int(maxBatch), C.int(windowMicros), &b); rc != C.BLBRS_OK {
+		return mapErr(rc)
+	}
+	if !batcher.CompareAndSwap(nil, b) {
+		C.blbrs_batcher_free(b)
+		return errors.New("rsgpu: batching already enabled")
+	}
+	return nil
+}
+
+// ChecksumBlocks returns crc32.Checksum(block, castagnoliTable) for every `block`-byte block
+// of b (block 0 = the whole buffer): the 65532-byte ChecksumFile blocks of
+// pkg/disk/checksum_block.go:18-34 and the bulk frame CRC of pkg/rpc/bulk_codec.go:47,
+// computed on the GPU (blb_rs.h: blbrs_crc32c).
+func ChecksumBlocks(b []byte, block int) ([]uint32, error) {
+	if len(b) == 0 {
+		return nil, nil
+	}
+	if block <= 0 {
+		block = len(b)
+	}
+	out := make([]uint32, (len(b)+block-1)/block)
+	var pin runtime.Pinner
+	pin.Pin(&b[0])
+	pin.Pin(&out[0])
+	defer pin.Unpin()
+	rc := C.blbrs_crc32c((*C.uint8_t)(unsafe.Pointer(&b[0])), C.size_t(len(b)), C.size_t(block),
+		(*C.uint32_t)(unsafe.Pointer(&out[0])))
+	return out, mapErr(rc)
+}
 
 // Map the C ABI's codes (blb_rs.h) back onto klauspost's exported error values, so
 // callers comparing against reedsolomon.ErrTooFewShards etc. keep working.
@@ -72,6 +113,9 @@ func New(dataShards, parityShards int) (reedsolomon.Encoder, error) {
 	if err != nil {
 		C.blbrs_free(h)
 		return nil, err
+	}
+	if b := batcher.Load(); b != nil {
+		C.blbrs_encoder_set_batcher(h, b)
 	}
 	e := &encoder{h: h, k: dataShards, m: parityShards, cpu: cpu}
 	runtime.SetFinalizer(e, func(e *encoder) { C.blbrs_free(e.h) })

@@ -26,6 +26,23 @@ int main(int argc, char** argv) {
     const int T = argc > 1 ? std::atoi(argv[1]) : 64;
     const int R = argc > 2 ? std::atoi(argv[2]) : 50;
     const int k = 6, m = 3, n = k + m;
+    {  // cost of the per-shard pointer classification under T-way contention
+        uint8_t* p = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), 1 << 20, hipHostMallocDefault) != hipSuccess) return 1;
+        const int N = 20000;
+        std::vector<std::thread> th;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                hipPointerAttribute_t a;
+                for (int i = 0; i < N; ++i) (void)hipPointerGetAttributes(&a, p + (t * 64 + i) % (1 << 20));
+            });
+        for (auto& x : th) x.join();
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("{\"probe\": \"hipPointerGetAttributes\", \"threads\": %d, \"calls_per_s\": %.0f}\n", T,
+                    T * static_cast<double>(N) / el);
+        (void)hipHostFree(p);
+    }
     for (size_t L : {size_t{4} << 10, size_t{16} << 10, size_t{64} << 10, size_t{256} << 10, size_t{1} << 20}) {
         // Per-thread pinned stripe + output.
         std::vector<uint8_t*> bufs(static_cast<size_t>(T) * (n + 1));
