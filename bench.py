@@ -94,11 +94,25 @@ def cpu_baseline(k, m, seconds):
         if el >= seconds:
             break
     gibps = done * k * TRACT / GIB / el
-    return {"value": round(gibps, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "avx2": bool(O.lib().rso_have_avx2()),
-            "sample": f"RS({k},{m}) encode of {done} stripes x {k}x8MiB "
-                      f"({done * k * TRACT / GIB:.1f} GiB data, {el:.1f} s) by the oracle's "
-                      f"klauspost-AVX2 restatement, {threads} OpenMP threads"}
+    out = {"value": round(gibps, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "avx2": bool(O.lib().rso_have_avx2()),
+           "sample": f"RS({k},{m}) encode of {done} stripes x {k}x8MiB "
+                     f"({done * k * TRACT / GIB:.1f} GiB data, {el:.1f} s) by the oracle's "
+                     f"klauspost-AVX2 restatement, {threads} OpenMP threads"}
+    # CRC-32C row: Go's amd64 algorithm class (SSE4.2, 3 interleaved streams), 65532-byte
+    # ChecksumFile blocks of m parity rows, ~3 s.
+    if O.lib().rso_have_sse42():
+        buf = rng.integers(0, 256, m * TRACT, dtype=np.uint8)
+        O.crc32c_blocks_hw(buf, 65532, threads)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < min(3.0, seconds):
+            O.crc32c_blocks_hw(buf, 65532, threads)
+            done += 1
+        el = time.perf_counter() - t0
+        out["crc32c"] = {"value": round(done * buf.size / el / 1e9, 2), "unit": "GB/s", "cores": threads,
+                         "kind": "port", "sample": f"{done} x CRC-32C of {m}x8MiB in 65532-byte blocks "
+                                                   f"({el:.1f} s), SSE4.2 3-stream, {threads} OpenMP threads"}
+    return out
 
 
 def main():

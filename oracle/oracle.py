@@ -64,6 +64,9 @@ def lib() -> ctypes.CDLL:
         L.rso_crc32c_update.restype = ctypes.c_uint32
         L.rso_crc32c_blocks.argtypes = [P, ctypes.c_size_t, ctypes.c_size_t, P]
         L.rso_crc32c_blocks.restype = None
+        L.rso_crc32c_blocks_hw.argtypes = [P, ctypes.c_size_t, ctypes.c_size_t, P, ctypes.c_int]
+        L.rso_crc32c_blocks_hw.restype = None
+        L.rso_have_sse42.restype = ctypes.c_int
         L.rso_have_avx2.restype = ctypes.c_int
         L.rso_max_threads.restype = ctypes.c_int
         _lib = L
@@ -143,4 +146,14 @@ def crc32c_blocks(data: np.ndarray, block: int) -> np.ndarray:
     nb = (a.size + block - 1) // block
     out = np.zeros(max(nb, 1), np.uint32)
     lib().rso_crc32c_blocks(a.ctypes.data, a.size, block, out.ctypes.data)
+    return out[:nb]
+
+
+def crc32c_blocks_hw(data: np.ndarray, block: int, threads: int = 1) -> np.ndarray:
+    """Go's amd64 CRC-32C algorithm class (SSE4.2, three interleaved streams) over OpenMP
+    threads: bench.py's CPU baseline for the CRC row.  Same output as crc32c_blocks."""
+    a = np.ascontiguousarray(data, dtype=np.uint8)
+    nb = (a.size + block - 1) // block
+    out = np.zeros(max(nb, 1), np.uint32)
+    lib().rso_crc32c_blocks_hw(a.ctypes.data, a.size, block, out.ctypes.data, int(threads))
     return out[:nb]

@@ -105,3 +105,18 @@ def test_gpu_crc32c_aligned_shapes(oracle_lib):
         for r in range(batch):
             want = oracle_lib.crc32c_blocks(host[r, :n], blk or n)
             assert np.array_equal(got[r], want), (blk, n, r)
+
+
+def test_oracle_crc32c_hw_equals_table(oracle_lib):
+    """The CPU-baseline restatement of Go's SSE4.2 path (three interleaved 8 KiB streams)
+    returns exactly the table oracle's CRCs."""
+    from oracle import oracle as O
+    if not O.lib().rso_have_sse42():
+        pytest.skip("no SSE4.2 on this host")
+    rng = np.random.default_rng(17)
+    for n, block in [(1, 1), (7, 0), (24575, 0), (24576, 0), (24577, 0), (3 * 65532 + 9, 65532),
+                     (200_001, 4096), ((1 << 20) + 5, 0)]:
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        blk = block or n
+        assert np.array_equal(O.crc32c_blocks_hw(d, blk, threads=3), oracle_lib.crc32c_blocks(d, blk)), (n, blk)
+    assert O.crc32c_blocks_hw(np.frombuffer(b"123456789", np.uint8), 9)[0] == CHECK
