@@ -17,11 +17,14 @@
  *   - Encoder.ReconstructData  client/blb/reconstruct.go:173
  *
  * Pinning: the reference tree holds no golden RS vectors (its tests only round-trip via
- * Verify: internal/tractserver/store_test.go:810-814,875-878).  This restatement is
- * cross-checked against an independent numpy restatement (oracle/rs_numpy.py, which uses
- * carry-less multiplication instead of log/exp tables), against the Backblaze/klauspost
- * RS(4,2) anchor matrix, and against algebraic properties.  Parity bytes are therefore
- * "pinned by restatement", not by reference output.
+ * Verify: internal/tractserver/store_test.go:810-814,875-878).  The restatement is pinned
+ * by the dependency's own published known-answer tests (tests/golden/published_kat.json,
+ * tests/test_published_kat.py): TestOneEncode's fixed RS(5,5) parity bytes, TestGalois'
+ * galMultiply/galExp values, TestMatrixMultiply and TestMatrixInverse[2]; CRC-32C by Go's
+ * hash/crc32 Castagnoli golden table.  It is further cross-checked against an independent
+ * numpy restatement (oracle/rs_numpy.py, carry-less multiplication instead of log/exp
+ * tables), the Backblaze/klauspost RS(4,2) matrix and algebraic properties.  No output of
+ * the reference itself exists here (Go and the module are absent).
  *
  * Two compute paths, same results:
  *   rso_code_scalar   -- klauspost's pure-Go path: galMulSlice/galMulSliceXor over mulTable
