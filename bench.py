@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--shard", type=int, default=TRACT)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-extra", action="store_true", help="skip decode / PCIe side measurements")
+    p.add_argument("--backend", default="nccl",
+                   help="torch.distributed backend for the barrier/max-time collectives (nccl = RCCL); "
+                        "'gloo' with ranks sharing a GPU is a rehearsal of the N>1 path on a 1-GPU box")
     return p.parse_args()
 
 
@@ -115,16 +118,86 @@ def cpu_baseline(k, m, seconds):
     return out
 
 
+def timed_all_ranks(fn, iters, dev, dist):
+    """Wall time of `iters` calls of fn on every rank, bracketed by barrier + sync on both
+    sides, max over ranks (the same clock discipline as the headline measurement)."""
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    return multigpu.max_over_ranks(time.perf_counter() - t0, dev)
+
+
+def scale_extras(enc, k, m, S, world, rank, dev, dist):
+    """BASELINE configs 4 and 5 at the job's N (run on every rank, aggregated over ranks):
+
+    * config 4 -- RS(10,4) Encode, then Reconstruct of 2 erasures (data 1 + data 7), 512
+      stripes per GPU: at N=8 that is exactly the batch=4096 split across 8 GPUs;
+    * config 5 -- RS(k,m) Encode of pinned host-resident stripes (PCIe-inclusive: the kernel
+      reads data and writes parity in host memory over PCIe), 24 stripes per GPU.
+
+    Totals are all ranks' data bytes / the max-over-ranks wall time."""
+    out = {}
+    per = 512
+    st = torch.empty((per, 14, S), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(97531 * (rank + 11))
+    st[:, :10].random_(0, 256, generator=g)
+    e104 = rs.New(10, 4)
+    e104.EncodeBatch(st)
+    ok = bool(e104.VerifyBatch(st).all())
+    t_enc = timed_all_ranks(lambda: e104.EncodeBatch(st), 3, dev, dist)
+    present = [i not in (1, 7) for i in range(14)]
+    st[:, 1].fill_(0xA5)  # really erase: the timed reconstructs must restore these bytes
+    st[:, 7].fill_(0x5A)
+    e104.ReconstructBatch(st, present, data_only=False)
+    t_rec = timed_all_ranks(lambda: e104.ReconstructBatch(st, present, data_only=False), 3, dev, dist)
+    ok = ok and bool(e104.VerifyBatch(st).all())
+    data_all = per * world * 10 * S * 3
+    out["config4_rs104_encode_reconstruct2"] = {
+        "stripes_total": per * world, "stripes_per_gpu": per,
+        "encode_GiBps_data": round(data_all / GIB / t_enc, 1),
+        "reconstruct2_GiBps_data": round(data_all / GIB / t_rec, 1),
+        "encode_ms": round(t_enc / 3 * 1e3, 3), "reconstruct2_ms": round(t_rec / 3 * 1e3, 3),
+        "verify_ok": ok}
+    del st
+    torch.cuda.empty_cache()
+
+    nb = 24
+    pinned = torch.empty((nb, k + m, S), dtype=torch.uint8).pin_memory()
+    pinned[:, :k].copy_(torch.randint(0, 256, (nb, k, S), dtype=torch.uint8, device=dev, generator=g))
+    host = pinned.numpy()
+    lists = [[host[b, i] for i in range(k + m)] for b in range(nb)]
+    enc.EncodeHostBatch(lists)
+    t_host = timed_all_ranks(lambda: enc.EncodeHostBatch(lists), 2, dev, dist)
+    out["config5_pcie_inclusive_encode"] = {
+        "GiBps_data": round(nb * world * k * S * 2 / GIB / t_host, 2), "stripes_per_gpu": nb,
+        "note": "pinned host stripes coded in place over PCIe (zero-copy: data read and parity "
+                "written in host memory by the kernel); not the bench value"}
+    del pinned
+    return out
+
+
 def main():
     a = parse()
     r = multigpu.env_rank()
     world, rank, local = r.world, r.rank, r.local
+    local = local % max(1, torch.cuda.device_count())  # identity on a node with >= N GPUs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.backend)
 
     k, m, S = a.k, a.m, a.shard
     if a.total_batch:
@@ -251,20 +324,12 @@ def main():
                                 "pieces": B * k, "tracts": sum(len(e) for e in per_col),
                                 "bytes_read": read_bytes, "bytes_written": B * k * S}
         del pool, per_col
-        # BASELINE config 5 shape on one GPU: PCIe-inclusive streaming from pinned host.
-        nb = 16
-        pinned = torch.empty((nb, k + m, S), dtype=torch.uint8).pin_memory()
-        pinned[:, :k].copy_(stripes[:nb, :k].cpu())
-        host = pinned.numpy()
-        lists = [[host[b, i] for i in range(k + m)] for b in range(nb)]
-        enc.EncodeHostBatch(lists, nstreams=3)
-        t1 = time.perf_counter()
-        enc.EncodeHostBatch(lists, nstreams=3)
-        el = time.perf_counter() - t1
-        extra["pcie_inclusive_encode"] = {
-            "GiBps_data": round(nb * k * S / GIB / el, 2), "stripes": nb,
-            "note": "pinned host -> H2D -> kernel -> D2H, 3 streams; not the bench value"}
-        del pinned
+
+    if not a.no_extra and a.shard == TRACT:
+        del stripes
+        torch.cuda.empty_cache()
+        extra.update(scale_extras(enc, k, m, S, world, rank, dev, dist))
+    if rank == 0 and world == 1 and not a.no_extra:
         cpu = cpu_baseline(k, m, a.cpu_seconds)
 
     if rank == 0:

@@ -32,13 +32,19 @@ def stripe_range(total: int, world: int, rank: int) -> tuple[int, int]:
     return start, base + (1 if rank < extra else 0)
 
 
+def _coll_device(device):
+    """Where the scalar all-reduce runs: the rank's GPU under RCCL, the CPU under gloo."""
+    import torch.distributed as dist
+    return "cpu" if dist.get_backend() == "gloo" else device
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """All-reduce MAX of a per-rank wall time (identity when not distributed)."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -49,7 +55,7 @@ def sum_over_ranks(value: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
