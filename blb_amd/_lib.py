@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libblbrs.so")
+LIB_PATH = os.environ.get("BLBRS_LIB_PATH") or os.path.join(HERE, "libblbrs.so")  # override: tuning builds
 
 # Every symbol include/blb_rs.h declares, with its ctypes signature.
 _P = ctypes.c_void_p
@@ -34,6 +34,7 @@ SIGNATURES = {
     "blbrs_encode_host_batch": (_I, [_P, _P, _SZ, _SZ, _I]),
     "blbrs_crc32c_dev": (_I, [_P, _SZ, _SZ, _SZ, _SZ, _P, _P]),
     "blbrs_crc32c": (_I, [_P, _SZ, _SZ, _P]),
+    "blbrs_encode_crc_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _SZ, _P, _P]),
     "blbrs_pack_dev": (_I, [_P, _SZ, _SZ, _SZ, _P, _SZ, _P]),
     "blbrs_batcher_new": (_I, [_I, _I, ctypes.POINTER(_P)]),
     "blbrs_batcher_free": (None, [_P]),

@@ -31,6 +31,7 @@
 
 #include "../../include/blb_rs.h"
 #include "crc32c.hpp"
+#include "encode_crc.hpp"
 #include "pack.hpp"
 #include "gf256.hpp"
 #include "rs_kernels.hpp"
@@ -1108,6 +1109,54 @@ int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t le
     if (block == 0) block = len;
     hipError_t e = crc32c_blocks(data, stride, batch, len, block, out_dev, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "crc32c_blocks");
+    return BLBRS_OK;
+}
+
+int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                         size_t batch, size_t shard_len, size_t block, uint32_t* crc_out_dev, void* stream) {
+    if (!enc || !crc_out_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (batch == 0 || shard_len == 0) return BLBRS_OK;
+    if (batch > 0x7FFFFFFFull) return fail(BLBRS_ERR_INVALID_ARG, "batch too large");
+    Stripes st;
+    int rc = dev_stripes_strided(enc, stripes, shard_stride, stripe_stride, batch, shard_len, &st);
+    if (rc) return rc;
+    int dev = 0;
+    if ((rc = current_dev_or_fail(&dev))) return rc;
+    auto hp = enc->encode_plan();
+    const DevPlan* plan = nullptr;
+    if ((rc = enc->dev_plan("E", *hp, dev, &plan))) return rc;
+    if (block == 0 || block > shard_len) block = shard_len;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    if (plan->passes.size() == 1) {
+        const DevPass& ps = plan->passes[0];
+        EncodeCrcArgs a{};
+        a.tables = ps.tables;
+        a.in_idx = ps.in_idx;
+        a.out_idx = ps.out_idx;
+        a.base = stripes;
+        a.shard_stride = shard_stride;
+        a.stripe_stride = stripe_stride;
+        a.B = static_cast<uint32_t>(batch);
+        a.S = shard_len;
+        a.block = block;
+        a.k = ps.k_in;
+        a.rows = ps.rows;
+        a.crc = crc_out_dev;
+        if (encode_crc_supported(a)) {
+            const hipError_t e = launch_encode_crc(a, s);
+            if (e != hipSuccess) return hip_fail(e, "launch encode_crc_kernel");
+            return BLBRS_OK;
+        }
+    }
+    // Shapes without a fused instantiation (or unaligned): the coding pass, then the CRC of
+    // each parity row -- same results, one more read of the parity.
+    if ((rc = run_plan(*plan, st, batch, shard_len, Mode::kStore, nullptr, s))) return rc;
+    const size_t nblocks = (shard_len + block - 1) / block;
+    for (int j = 0; j < enc->m; ++j) {
+        const hipError_t e = crc32c_blocks(stripes + static_cast<size_t>(enc->k + j) * shard_stride, stripe_stride,
+                                           batch, shard_len, block, crc_out_dev + j * batch * nblocks, s);
+        if (e != hipSuccess) return hip_fail(e, "crc32c_blocks");
+    }
     return BLBRS_OK;
 }
 

@@ -1,9 +1,6 @@
-// crc32c.hip -- CRC-32C (Castagnoli) of shard blocks on gfx950 (see crc32c.hpp).
+// crc32c.hip -- CRC-32C (Castagnoli) of shard blocks on gfx950 (see crc32c.hpp; the raw-CRC
+// algebra, S_n shift matrices and banked LDS tables are in crc_device.hpp).
 //
-// CRC is linear over GF(2).  With raw(M) = the register after feeding M into a zero
-// register (no init, no final xor):
-//     raw(A || B) = S_{|B|} raw(A)  ^  raw(B)          S_n = "feed n zero bytes", a 32x32
-//     crc(M)      = ~( S_{|M|} 0xFFFFFFFF ^ raw(M) )   GF(2) matrix (host-precomputed).
 // Kernel 1 (one workgroup per <= 64 KiB segment): the segment is staged in LDS behind a
 // zero prefix so that 256 lanes each own exactly L = C*Lc bytes (leading zeros do not
 // change raw).  Each lane runs C = 4 independent slicing-by-4 chains over its C adjacent
@@ -15,6 +12,7 @@
 // the init term.  CRC is computed byte-serially per lane, so this is LDS/VALU work, not
 // a streaming HBM kernel; it runs beside the coding kernel on the data it just wrote.
 #include "crc32c.hpp"
+#include "crc_device.hpp"
 
 #include <map>
 #include <mutex>
@@ -23,41 +21,11 @@
 namespace blbrs {
 namespace {
 
+using namespace dev;
+using V4x = u32x4;
+
 constexpr int kThreads = 256;
-constexpr uint32_t kPoly = 0x82F63B78u;  // reflected Castagnoli
-constexpr int kPow2 = 48;                // S_{2^i}, i < 48
-
-// Device constants for one (L, SEG) configuration.
-struct CrcConsts {
-    uint32_t table[4][256];     // slicing-by-4 tables
-    uint32_t chain[3][32];      // S_{(3-j) * Lc}: chain j -> end of the lane's region
-    uint32_t lvl[8][32];        // S_{L * 2^j}, columns
-    uint32_t seg[32];           // S_SEG
-    uint32_t pow2[kPow2][32];   // S_{2^i}
-    // streaming kernel (crc_stream_kernel): 16-byte lane chunks in 1 KiB rows
-    uint32_t gap[32];           // S_4032: from the end of a lane's chunk to its next chunk
-    uint32_t wlvl[6][32];       // S_{64 * 2^j}: lane folds inside a wave
-};
-
-using cu32 = const uint32_t __attribute__((address_space(4)))*;
-using V4x = uint32_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ cu32 as_const(const uint32_t* p) { return (cu32)(uintptr_t)p; }
-
-// r -> S r for a column-major 32x32 GF(2) matrix held in constant memory (scalar loads):
-// per bit, a 1-bit sign-extract and one v_bitop3 (out ^ (mask & col), truth table 0x78).
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-__device__ __forceinline__ uint32_t apply(cu32 col, uint32_t r) {
-    uint32_t out = 0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        const uint32_t mask = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(r), i, 1));
-        out = __builtin_amdgcn_bitop3_b32(out, mask, col[i], 0x78);
-    }
-    return out;
-}
+constexpr int kPow2 = kCrcPow2;
 
 struct SegArgs {
     const uint8_t* data;
@@ -174,7 +142,7 @@ __global__ __launch_bounds__(kThreads) void crc_segment_kernel(SegArgs a) {
 constexpr int kStreamThreads = 1024;
 constexpr uint32_t kChunk = 64, kRowBytes = kChunk * 64, kRows = 16;  // 4 KiB rows
 constexpr uint32_t kWaveSeg = kRowBytes * kRows;                      // 64 KiB per wave
-constexpr size_t kStreamLds = 4u * 256u * 32u * 4u;                   // 128 KiB
+constexpr size_t kStreamLds = kBankedTableBytes;                       // 128 KiB
 
 struct StreamArgs {
     const uint8_t* data;
@@ -188,24 +156,6 @@ struct StreamArgs {
 struct Chunk {
     V4x q[4];
 };
-
-// Table lookups for byte k of x: table 3-k (crc32c_le slicing order).  The kernel has no
-// static LDS, so its dynamic LDS starts at address 0 and a perm result IS the LDS address.
-struct LaneTabs {
-    uint32_t b[4];  // LDS address of this lane's bank in the table serving byte k
-};
-
-typedef const __attribute__((address_space(3))) uint32_t* lds_u32;
-
-template <uint32_t K>
-__device__ __forceinline__ uint32_t lookup(const LaneTabs& t, uint32_t x) {
-    constexpr uint32_t sel = 0x03020000u | ((4u + K) << 8);  // [base.b0, x.bK, base.b2, base.b3]
-    return *reinterpret_cast<lds_u32>(static_cast<size_t>(__builtin_amdgcn_perm(x, t.b[K], sel)));
-}
-
-__device__ __forceinline__ uint32_t slice4(const LaneTabs& t, uint32_t x) {
-    return xor3(lookup<0>(t, x), lookup<1>(t, x), lookup<2>(t, x)) ^ lookup<3>(t, x);
-}
 
 __device__ __forceinline__ uint32_t crc_chunk(const LaneTabs& t, uint32_t c, const Chunk& ch) {
 #pragma unroll
@@ -233,23 +183,15 @@ __device__ __forceinline__ Chunk load_row(const uint8_t* p) {
 __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void crc_stream_kernel(
     StreamArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
-    for (uint32_t i = threadIdx.x; i < 4u * 256u * 32u; i += kStreamThreads) {
-        const uint32_t j = ((i >> 14) << 1) | ((i >> 5) & 1u), e = (i >> 6) & 255u;
-        tab[i] = a.c->table[j][e];
-    }
+    init_banked_tables(tab, a.c, kStreamThreads);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
-    LaneTabs t;
-    const uint32_t lb = (lane & 31u) << 2;
-    t.b[0] = (1u << 16) | (1u << 7) | lb;  // table 3
-    t.b[1] = (1u << 16) | lb;              // table 2
-    t.b[2] = (1u << 7) | lb;               // table 1
-    t.b[3] = lb;                           // table 0
+    const LaneTabs t(lane);
     const uint64_t waves = static_cast<uint64_t>(gridDim.x) * (kStreamThreads / 64);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const cu32 gap = as_const(a.c->gap);
-    const cu32 wlvl = as_const(&a.c->wlvl[0][0]);
+    const cu32 gap = as_const(a.c->gap[0]);
+    const cu32 wlvl = as_const(&a.c->wlvl[0][0][0]);
     for (uint64_t g = blockIdx.x * (kStreamThreads / 64) + wave; g < a.total_segs; g += waves) {
         const uint32_t s = static_cast<uint32_t>(g % a.segs_per_block);
         const uint32_t blk = static_cast<uint32_t>((g / a.segs_per_block) % a.nblocks);
@@ -389,7 +331,7 @@ void build_consts(uint64_t seg, CrcConsts* c) {
     const uint32_t L = kLaneDw * 4, Lc = kChainDw * 4;
     for (uint32_t i = 0; i < 256; ++i) {
         uint32_t v = i;
-        for (int j = 0; j < 8; ++j) v = (v & 1u) ? (v >> 1) ^ kPoly : v >> 1;
+        for (int j = 0; j < 8; ++j) v = (v & 1u) ? (v >> 1) ^ kCrcPoly : v >> 1;
         c->table[0][i] = v;
     }
     for (int k = 1; k < 4; ++k)
@@ -409,18 +351,23 @@ void build_consts(uint64_t seg, CrcConsts* c) {
     }
     const Mat32 ms = mat_pow(p, seg);
     for (int j = 0; j < 32; ++j) c->seg[j] = ms.col[j];
-    const Mat32 mg = mat_pow(p, kRowBytes - kChunk);
-    for (int j = 0; j < 32; ++j) c->gap[j] = mg.col[j];
-    for (int l = 0; l < 6; ++l) {
-        const Mat32 m = mat_pow(p, uint64_t{kChunk} << l);
-        for (int j = 0; j < 32; ++j) c->wlvl[l][j] = m.col[j];
+    for (int v = 0; v < 2; ++v) {  // lane chunks of LC = 64 (v = 0) and 32 (v = 1) bytes
+        const uint64_t lc = v == 0 ? 64 : 32;
+        const Mat32 mg = mat_pow(p, 64 * lc - lc);
+        for (int j = 0; j < 32; ++j) c->gap[v][j] = mg.col[j];
+        for (int l = 0; l < 6; ++l) {
+            const Mat32 m = mat_pow(p, lc << l);
+            for (int j = 0; j < 32; ++j) c->wlvl[v][l][j] = m.col[j];
+        }
     }
 }
 
 std::mutex g_mu;
 std::map<std::pair<int, uint64_t>, CrcConsts*> g_consts;  // device copies, process lifetime
 
-hipError_t consts_for(uint64_t seg, const CrcConsts** out) {
+}  // namespace
+
+hipError_t crc_consts_for(uint64_t seg, const CrcConsts** out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -441,7 +388,21 @@ hipError_t consts_for(uint64_t seg, const CrcConsts** out) {
     return hipSuccess;
 }
 
-}  // namespace
+hipError_t crc_combine(const CrcConsts* c, const uint32_t* raw, uint64_t len, uint64_t block, uint64_t seg,
+                       uint32_t nblocks, uint32_t segs_per_block, uint64_t total_blocks, uint32_t* out,
+                       hipStream_t stream) {
+    SegArgs a{};
+    a.len = len;
+    a.block = block;
+    a.seg = seg;
+    a.nblocks = nblocks;
+    a.segs_per_block = segs_per_block;
+    a.c = c;
+    a.raw = const_cast<uint32_t*>(raw);
+    hipLaunchKernelGGL(crc_combine_kernel, dim3(static_cast<unsigned>((total_blocks + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, stream, a, total_blocks, out);
+    return hipGetLastError();
+}
 
 hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, uint64_t len, uint64_t block,
                          uint32_t* out, hipStream_t stream) {
@@ -454,7 +415,7 @@ hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, u
                            (block & 3u) == 0 && (len & 3u) == 0;
     const uint64_t seg = stream_ok ? kWaveSeg : (block < kSegMax ? block : kSegMax);
     const CrcConsts* c = nullptr;
-    hipError_t e = consts_for(seg, &c);
+    hipError_t e = crc_consts_for(seg, &c);
     if (e != hipSuccess) return e;
     SegArgs a{};
     a.data = data;
@@ -488,11 +449,8 @@ hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, u
                            stream, a);
     }
     e = hipGetLastError();
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(crc_combine_kernel, dim3(static_cast<unsigned>((total_blocks + kThreads - 1) / kThreads)),
-                           dim3(kThreads), 0, stream, a, total_blocks, out);
-        e = hipGetLastError();
-    }
+    if (e == hipSuccess)
+        e = crc_combine(c, a.raw, len, block, seg, a.nblocks, a.segs_per_block, total_blocks, out, stream);
     hipError_t f = hipFreeAsync(a.raw, stream);
     return e != hipSuccess ? e : f;
 }

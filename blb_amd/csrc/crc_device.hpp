@@ -1,0 +1,90 @@
+// crc_device.hpp -- CRC-32C (Castagnoli) building blocks shared by the CRC kernels
+// (crc32c.hip) and the fused encode+CRC kernel (encode_crc.hip).
+//
+// CRC is linear over GF(2).  With raw(M) = the register after feeding M into a zero
+// register (no init, no final xor):
+//     raw(A || B) = S_{|B|} raw(A)  ^  raw(B)          S_n = "feed n zero bytes", a 32x32
+//     crc(M)      = ~( S_{|M|} 0xFFFFFFFF ^ raw(M) )   GF(2) matrix (host-precomputed).
+#pragma once
+#include "dev_common.hpp"
+
+namespace blbrs {
+
+constexpr uint32_t kCrcPoly = 0x82F63B78u;  // reflected Castagnoli
+constexpr int kCrcPow2 = 48;                // S_{2^i}, i < 48
+
+// Device constants for one segment size (host-built once per (device, seg)).
+struct CrcConsts {
+    uint32_t table[4][256];        // slicing-by-4 tables
+    uint32_t chain[3][32];         // S_{(3-j) * Lc}: chain j -> end of the lane's region
+    uint32_t lvl[8][32];           // S_{L * 2^j}, columns
+    uint32_t seg[32];              // S_SEG
+    uint32_t pow2[kCrcPow2][32];   // S_{2^i}
+    // streaming kernels: lane chunks of LC bytes at column lane of 64*LC-byte rows
+    uint32_t gap[2][32];           // S_{64*LC - LC} for LC = 64, 32: chunk end -> next chunk
+    uint32_t wlvl[2][6][32];       // S_{LC * 2^j} for LC = 64, 32: lane folds inside a wave
+};
+
+// Per-segment raw CRCs -> per-block CRCs: block id of `total_blocks` (= rows * nblocks; row
+// r's block j is id r * nblocks + j) folds its raw[id * segs_per_block + s] with S_seg
+// (Horner) and applies the init term.  out[id] = crc32.Checksum(block).
+hipError_t crc_consts_for(uint64_t seg, const CrcConsts** out);
+hipError_t crc_combine(const CrcConsts* c, const uint32_t* raw, uint64_t len, uint64_t block, uint64_t seg,
+                       uint32_t nblocks, uint32_t segs_per_block, uint64_t total_blocks, uint32_t* out,
+                       hipStream_t stream);
+
+namespace dev {
+
+// r -> S r for a column-major 32x32 GF(2) matrix held in constant memory (scalar loads):
+// per bit, a 1-bit sign-extract and one v_bitop3 (out ^ (mask & col), truth table 0x78).
+__device__ __forceinline__ uint32_t apply(cu32 col, uint32_t r) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t mask = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(r), i, 1));
+        out = __builtin_amdgcn_bitop3_b32(out, mask, col[i], 0x78);
+    }
+    return out;
+}
+
+// Banked slicing tables in LDS (128 KiB): a private copy of the four tables per bank, laid
+// out so table j, entry e, bank l lives at byte (j>>1)<<16 | e<<8 | (j&1)<<7 | l<<2.  A
+// 32-lane group then always hits 32 distinct banks and each lookup address is ONE v_perm_b32
+// of (x, base_j).  The kernel must have no static LDS, so its dynamic LDS starts at address
+// 0 and a perm result IS the LDS address.
+constexpr size_t kBankedTableBytes = 4u * 256u * 32u * 4u;
+
+__device__ __forceinline__ void init_banked_tables(uint32_t* tab, const CrcConsts* c, uint32_t nthreads) {
+    for (uint32_t i = threadIdx.x; i < 4u * 256u * 32u; i += nthreads) {
+        const uint32_t j = ((i >> 14) << 1) | ((i >> 5) & 1u), e = (i >> 6) & 255u;
+        tab[i] = c->table[j][e];
+    }
+}
+
+struct LaneTabs {
+    uint32_t b[4];  // LDS address of this lane's bank in the table serving byte k
+    __device__ __forceinline__ explicit LaneTabs(uint32_t lane) {
+        const uint32_t lb = (lane & 31u) << 2;
+        b[0] = (1u << 16) | (1u << 7) | lb;  // table 3
+        b[1] = (1u << 16) | lb;              // table 2
+        b[2] = (1u << 7) | lb;               // table 1
+        b[3] = lb;                           // table 0
+    }
+};
+
+typedef const __attribute__((address_space(3))) uint32_t* lds_u32;
+
+// Table lookups for byte k of x: table 3-k (crc32c_le slicing order).
+template <uint32_t K>
+__device__ __forceinline__ uint32_t lookup(const LaneTabs& t, uint32_t x) {
+    constexpr uint32_t sel = 0x03020000u | ((4u + K) << 8);  // [base.b0, x.bK, base.b2, base.b3]
+    return *reinterpret_cast<lds_u32>(static_cast<size_t>(__builtin_amdgcn_perm(x, t.b[K], sel)));
+}
+
+// raw(c || w) for one dword w: slicing-by-4 (4 perms + 4 LDS reads + 2 XOR).
+__device__ __forceinline__ uint32_t slice4(const LaneTabs& t, uint32_t x) {
+    return xor3(lookup<0>(t, x), lookup<1>(t, x), lookup<2>(t, x)) ^ lookup<3>(t, x);
+}
+
+}  // namespace dev
+}  // namespace blbrs

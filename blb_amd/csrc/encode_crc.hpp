@@ -1,0 +1,31 @@
+// encode_crc.hpp -- fused RS encode + CRC-32C of the parity it writes (encode_crc.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace blbrs {
+
+// One pass over HBM: parity rows out[j] = XOR_c coef[j][c] * in[c] of every stripe are
+// stored, and CRC-32C of every `block`-byte block of every parity shard is written to
+// crc[(j * B + b) * nblocks + i] (Go's crc32.Checksum with the Castagnoli table).
+struct EncodeCrcArgs {
+    const uint32_t* tables;   // device: [rows][k][5] v_perm words (the encode pass)
+    const int32_t* in_idx;    // device: [k]
+    const int32_t* out_idx;   // device: [rows]
+    uint8_t* base;            // strided stripes: shard i of stripe b at base + b*stripe_stride + i*shard_stride
+    uint64_t shard_stride, stripe_stride;
+    uint32_t B;
+    uint64_t S;               // shard length
+    uint64_t block;           // CRC block length (<= S)
+    int32_t k, rows;
+    uint32_t* crc;            // device: [rows][B][nblocks]
+};
+
+// True when the fused kernel covers this shape: an instantiated (k, rows), 4-byte aligned
+// base/strides/length/block.  Otherwise the caller runs the coding pass and crc32c_blocks.
+bool encode_crc_supported(const EncodeCrcArgs& a);
+
+// Launches the fused kernel plus the per-block combine on `stream`.
+hipError_t launch_encode_crc(const EncodeCrcArgs& a, hipStream_t stream);
+
+}  // namespace blbrs

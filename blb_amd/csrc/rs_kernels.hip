@@ -32,97 +32,12 @@
 
 #include <algorithm>
 
+#include "gf_device.hpp"
+
 namespace blbrs {
 namespace {
 
-struct alignas(16) V4 { uint32_t x, y, z, w; };
-
-// Read-only metadata (tables, shard indices, pointer tables) is read through the constant
-// address space so the compiler may use scalar (s_load) loads for it.
-using cu32 = const uint32_t __attribute__((address_space(4)))*;
-using ci32 = const int32_t __attribute__((address_space(4)))*;
-using cu64 = const uint64_t __attribute__((address_space(4)))*;
-__device__ __forceinline__ cu32 as_const(const uint32_t* p) { return (cu32)(uintptr_t)p; }
-__device__ __forceinline__ ci32 as_const(const int32_t* p) { return (ci32)(uintptr_t)p; }
-__device__ __forceinline__ cu64 as_const(const uint64_t* p) { return (cu64)(uintptr_t)p; }
-
-
-// 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96 = a ^ b ^ c); hipcc
-// does not form it from a ^ b ^ c by itself.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-// Bit groups of NV input dwords: g0 = x[2:0], g1 = x[5:3], g2 = x[7:6] of every byte
-// (5 VALU per dword, shared by every output row).
-template <int NV>
-struct Groups {
-    uint32_t g0[NV], g1[NV], g2[NV];
-    __device__ __forceinline__ explicit Groups(const uint32_t (&x)[NV]) {
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            g0[v] = x[v] & 0x07070707u;
-            g1[v] = (x[v] >> 3) & 0x07070707u;
-            g2[v] = (x[v] >> 6) & 0x03030303u;
-        }
-    }
-};
-
-template <typename TP>
-__device__ __forceinline__ void load_tab(TP tp, uint32_t (&t)[5]) {
-#pragma unroll
-    for (int w = 0; w < 5; ++w) t[w] = tp[w];
-}
-
-// acc[r] ^= coef(r, c) * x over NV input dwords of ONE input shard c: 3 v_perm + 2 xor3
-// ... per (row, dword).  Each row's 5 table words are fetched once and applied to all NV
-// dwords (amortises the SGPR->VGPR moves v_perm needs for its second table operand under
-// gfx9's one-SGPR constant-bus limit).
-template <int MR, int NV, typename Tab>
-__device__ __forceinline__ void madd(const Groups<NV>& g, Tab tab, uint32_t (&acc)[MR][NV], int nr) {
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-        if (r < nr) {
-            uint32_t t[5];
-            load_tab(tab(r), t);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const uint32_t p0 = __builtin_amdgcn_perm(t[1], t[0], g.g0[v]);
-                const uint32_t p1 = __builtin_amdgcn_perm(t[3], t[2], g.g1[v]);
-                const uint32_t p2 = __builtin_amdgcn_perm(0u, t[4], g.g2[v]);
-                acc[r][v] = xor3(xor3(acc[r][v], p0, p1), p2, 0u);
-            }
-        }
-    }
-}
-
-// Two input shards at once: 6 perm terms + acc folded by 3 xor3 (1.5 VALU per coefficient
-// and dword instead of 3 plain XORs).
-template <int MR, int NV, typename TabA, typename TabB>
-__device__ __forceinline__ void madd2(const Groups<NV>& ga, TabA taba, const Groups<NV>& gb, TabB tabb,
-                                      uint32_t (&acc)[MR][NV], int nr) {
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-        if (r < nr) {
-            uint32_t a[5], b[5];
-            load_tab(taba(r), a);
-            load_tab(tabb(r), b);
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const uint32_t a0 = __builtin_amdgcn_perm(a[1], a[0], ga.g0[v]);
-                const uint32_t a1 = __builtin_amdgcn_perm(a[3], a[2], ga.g1[v]);
-                const uint32_t a2 = __builtin_amdgcn_perm(0u, a[4], ga.g2[v]);
-                const uint32_t b0 = __builtin_amdgcn_perm(b[1], b[0], gb.g0[v]);
-                const uint32_t b1 = __builtin_amdgcn_perm(b[3], b[2], gb.g1[v]);
-                const uint32_t b2 = __builtin_amdgcn_perm(0u, b[4], gb.g2[v]);
-                acc[r][v] = xor3(xor3(xor3(acc[r][v], a0, a1), a2, b0), b1, b2);
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ void unpack(const V4& q, uint32_t* w) { w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w; }
-__device__ __forceinline__ V4 pack(const uint32_t* w) { return V4{w[0], w[1], w[2], w[3]}; }
+using namespace dev;
 
 template <int ADDR>
 __device__ __forceinline__ uint8_t* shard_ptr(const CodeArgs& a, uint32_t b, int idx) {
@@ -132,8 +47,6 @@ __device__ __forceinline__ uint8_t* shard_ptr(const CodeArgs& a, uint32_t b, int
     else
         return reinterpret_cast<uint8_t*>(as_const(a.ptrs)[static_cast<uint64_t>(b) * a.nshards + idx]);
 }
-
-using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
 
 // 16-byte global load/store; NT bit 0 = nontemporal loads, bit 1 = nontemporal stores
 // (streamed data is touched exactly once).

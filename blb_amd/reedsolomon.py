@@ -282,6 +282,23 @@ class Encoder:
         st = _torch_stream(stripes) if stream is None else stream
         _check(self._lib.blbrs_encode_dev(self._h, stripes.data_ptr(), ss, bs, B, S, st))
 
+    def EncodeBatchCRC(self, stripes, block: int = 0, stream: Optional[int] = None):
+        """EncodeBatch fused with the CRC-32C of the parity it writes (one HBM pass).
+
+        Returns a [m, B, nblocks] torch.int32 CUDA tensor (the uint32 CRCs' bit patterns):
+        entry [j, b, i] = crc32.Checksum(block i of parity shard k+j of stripe b).
+        block = 0: one block per shard (the bulk RPC frame CRC, pkg/rpc/bulk_codec.go:47);
+        65532 = ChecksumFile blocks (pkg/disk/checksum_block.go:18-34)."""
+        import torch
+        B, S, ss, bs = self._stripes(stripes)
+        blk = S if block <= 0 or block > S else block
+        nblocks = (S + blk - 1) // blk if S else 0
+        out = torch.empty((self.ParityShards, B, nblocks), dtype=torch.int32, device=stripes.device)
+        st = _torch_stream(stripes) if stream is None else stream
+        _check(self._lib.blbrs_encode_crc_dev(self._h, stripes.data_ptr(), ss, bs, B, S, blk,
+                                              out.data_ptr(), st))
+        return out
+
     def ReconstructBatch(self, stripes, present: Sequence[bool], data_only: bool = False,
                          stream: Optional[int] = None) -> None:
         """Rebuild the shards marked absent in `present` for every stripe, in place."""

@@ -139,6 +139,21 @@ int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t le
 /* Host-memory form: one buffer; out (host) has ceil(len / block) entries. */
 int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out);
 
+/* Encode fused with the CRC-32C of the parity it writes, in one pass over HBM: what
+ * Store.rsEncodeOne does with each increment (Encode, store.go:1099) followed by the
+ * checksum of every parity shard it ships -- the bulk RPC frame CRC of CtlWrite
+ * (pkg/rpc/bulk_codec.go:47; block = 0 = whole shard) or the receiver's ChecksumFile blocks
+ * (block = 65532, pkg/disk/checksum_block.go:18-34).  Same strided layout and parity bytes
+ * as blbrs_encode_dev; crc_out_dev (device) receives m * batch * nblocks entries,
+ * nblocks = ceil(shard_len / block):
+ *     crc_out_dev[(j * batch + b) * nblocks + i] = CRC-32C of block i of parity shard k+j
+ *                                                  of stripe b.
+ * Shapes without a fused kernel fall back to the coding pass plus blbrs_crc32c_dev's kernel
+ * (same results). */
+int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
+                         size_t stripe_stride, size_t batch, size_t shard_len, size_t block,
+                         uint32_t* crc_out_dev, void* stream);
+
 /* ---- batched client reconstructs ----
  * client/blb/reconstruct.go:65-195 calls ReconstructData once per degraded read (one stripe
  * of `length`-byte pieces), up to MaxInFlight (:19,35-45) at once.  A batcher collects
