@@ -102,6 +102,27 @@ def cpu_baseline(k, m, seconds):
            "sample": f"RS({k},{m}) encode of {done} stripes x {k}x8MiB "
                      f"({done * k * TRACT / GIB:.1f} GiB data, {el:.1f} s) by the oracle's "
                      f"klauspost-AVX2 restatement, {threads} OpenMP threads"}
+    # The other BASELINE rows on the same restatement (~2 s each).  Decode = the rows of
+    # inv(M[first k present]) for the erased data shards, applied to the k survivors.
+    def rate(kk, mm, missing, secs=2.0):
+        mat = O.build_matrix(kk, mm)
+        if missing:
+            valid = [i for i in range(kk + mm) if i not in missing][:kk]
+            rows_ = O.invert(mat[valid])[list(missing)]
+        else:
+            rows_ = mat[kk:]
+        ins = [rng.integers(0, 256, TRACT, dtype=np.uint8) for _ in range(kk)]
+        outs = [np.empty(TRACT, np.uint8) for _ in range(rows_.shape[0])]
+        O.code(rows_, ins, outs, use_avx2=True, threads=threads)
+        n, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < secs:
+            O.code(rows_, ins, outs, use_avx2=True, threads=threads)
+            n += 1
+        return round(n * kk * TRACT / GIB / (time.perf_counter() - t1), 2)
+    out["configs"] = {"unit": "GiB/s of data (k shards x 8 MiB per call)",
+                      "rs63_reconstruct_data1": rate(6, 3, [1]),
+                      "rs104_encode": rate(10, 4, []),
+                      "rs104_reconstruct_data1_data7": rate(10, 4, [1, 7])}
     # CRC-32C row: Go's amd64 algorithm class (SSE4.2, 3 interleaved streams), 65532-byte
     # ChecksumFile blocks of m parity rows, ~3 s.
     if O.lib().rso_have_sse42():
