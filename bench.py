@@ -111,11 +111,13 @@ def cpu_baseline(k, m, seconds):
             rows_ = O.invert(mat[valid])[list(missing)]
         else:
             rows_ = mat[kk:]
-        ins = [rng.integers(0, 256, TRACT, dtype=np.uint8) for _ in range(kk)]
-        outs = [np.empty(TRACT, np.uint8) for _ in range(rows_.shape[0])]
-        O.code(rows_, ins, outs, use_avx2=True, threads=threads)
+        # 4 stripes in rotation, like the encode sample: the working set is not cache-resident
+        sets = [([rng.integers(0, 256, TRACT, dtype=np.uint8) for _ in range(kk)],
+                 [np.empty(TRACT, np.uint8) for _ in range(rows_.shape[0])]) for _ in range(4)]
+        O.code(rows_, sets[0][0], sets[0][1], use_avx2=True, threads=threads)
         n, t1 = 0, time.perf_counter()
         while time.perf_counter() - t1 < secs:
+            ins, outs = sets[n % 4]
             O.code(rows_, ins, outs, use_avx2=True, threads=threads)
             n += 1
         return round(n * kk * TRACT / GIB / (time.perf_counter() - t1), 2)
