@@ -82,6 +82,21 @@ void run_pattern(int grid) {
     printf("pattern XCD=%d R=%d W=%d U=%d NT=%d grid=%6d : %8.3f ms  %7.1f GB/s\n", XCD, R, W, U, NT, grid, ms, bytes / ms / 1e6);
 }
 
+// Pattern ceiling at a wider shape: stripes of R+W shards packed back to back in the same
+// buffer (as shape() views it for rs_code_kernel), so the two are directly comparable.
+template <int R, int W, int U>
+void run_pattern_shape() {
+    const uint64_t ss = S, bs = uint64_t(R + W) * S;
+    const uint32_t nb = static_cast<uint32_t>(uint64_t(B) * 9 * S / bs);
+    const uint32_t tps = static_cast<uint32_t>(S / (4096 * U));
+    const int grid = static_cast<int>(nb * tps) & ~7;
+    double ms = time_ms([&] { hipLaunchKernelGGL((pattern_kernel<R, W, U, 3, 1>), dim3(grid), dim3(256), 0, 0,
+                                                 g_base, ss, bs, nb, tps, g_sink); });
+    const double bytes = double(nb) * (R + W) * S;
+    printf("pattern R=%2d W=%d U=%d B=%4u : %8.3f ms  %7.1f GB/s  %7.1f GiB/s data\n", R, W, U, nb, ms, bytes / ms / 1e6,
+           double(nb) * R * S / (ms * 1e-3) / double(1u << 30));
+}
+
 template <int U, int NT, int K = 6, int MR = 3, int MODE = 0>
 void run_rs(CodeArgs a, int grid, const char* tag, int remap = 0) {
     a.xcd_remap = remap;
@@ -174,7 +189,8 @@ int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "zc") { zero_copy_probe(); return 0; }
     const bool stride = argc > 1 && std::string(argv[1]) == "stride";
     const bool pmc = argc > 1 && std::string(argv[1]) == "pmc";
-    if (argc > 1 && !pmc && !stride) B = static_cast<uint32_t>(atoi(argv[1]));
+    const bool ceil = argc > 1 && std::string(argv[1]) == "ceil";
+    if (argc > 1 && !pmc && !stride && !ceil) B = static_cast<uint32_t>(atoi(argv[1]));
     const size_t total = size_t(B) * 9 * S;
     CK(hipMalloc(&g_base, total));
     CK(hipMalloc(&g_sink, 64));
@@ -225,6 +241,26 @@ int main(int argc, char** argv) {
         CK(hipDeviceSynchronize());
         printf("pmc launches done: read_bytes=%.0f copy_bytes=%.0f+%.0f rs63_bytes=%.0f+%.0f\n", double(B) * 9 * S,
                double(B) * S, double(B) * S, double(B) * 6 * S, double(B) * 3 * S);
+        return 0;
+    }
+    if (ceil) {
+        // Wide-shape question: is RS(10,4)/RS(12,5) below its own
+        // access-pattern ceiling, or is the ceiling itself lower than RS(6,3)'s?
+        for (int rep = 0; rep < 2; ++rep) {
+            printf("# ceil rep %d\n", rep);
+            run_pattern_shape<6, 3, 4>();
+            run_rs<4, 3>(a, 1, "all", 1);
+            run_pattern_shape<10, 4, 2>();
+            run_pattern_shape<10, 4, 4>();
+            run_rs<2, 3, 10, 4>(shape(10, 4), 1, "rs104", 1);
+            run_pattern_shape<12, 5, 2>();
+            run_pattern_shape<12, 5, 4>();
+            run_rs<2, 3, 12, 5>(shape(12, 5), 1, "rs125", 1);
+            run_pattern_shape<10, 2, 2>();
+            run_rs<2, 3, 10, 2>(shape(10, 2), 1, "dec2", 1);
+            run_pattern_shape<6, 1, 4>();
+            run_rs<4, 3, 6, 1>(shape(6, 1), 1, "dec1", 1);
+        }
         return 0;
     }
     for (int rep = 0; rep < 1; ++rep) {
