@@ -309,8 +309,10 @@ def main():
         crc_ms = crc_evs[0].elapsed_time(crc_evs[1])
         extra["crc32c_parity_blocks"] = {"GBps": round(B * m * S / (crc_ms * 1e-3) / 1e9, 1),
                                          "ms": round(crc_ms, 3), "bytes": B * m * S, "block": 65532}
-        # The same two steps fused (encode_crc_kernel): parity checksummed in registers.
-        for blk_name, blk in (("blocks65532", checksum.CHECKSUM_BLOCK_DATA), ("whole_shard", 0)):
+        # The same two steps fused: parity checksummed in registers.  Default = the tile-grid
+        # kernel (encode_crc_tile.hip); the persistent segment kernel (encode_crc.hip) is
+        # timed beside it for the A/B (BLBRS_EC_PERSISTENT, read per call).
+        def fused_ms(blk):
             enc.EncodeBatchCRC(stripes, blk)
             torch.cuda.synchronize(dev)
             f_evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -320,10 +322,19 @@ def main():
                 enc.EncodeBatchCRC(stripes, blk)
                 e.record(stream)
             torch.cuda.synchronize(dev)
-            f_ms = float(np.mean([s.elapsed_time(e) for s, e in f_evs]))
+            return float(np.mean([s.elapsed_time(e) for s, e in f_evs]))
+        for blk_name, blk in (("blocks65532", checksum.CHECKSUM_BLOCK_DATA), ("whole_shard", 0)):
+            f_ms = fused_ms(blk)
+            os.environ["BLBRS_EC_PERSISTENT"] = "1"
+            try:
+                p_ms = fused_ms(blk)
+            finally:
+                del os.environ["BLBRS_EC_PERSISTENT"]
             extra[f"encode_crc_fused_{blk_name}"] = {
                 "ms_per_launch": round(f_ms, 3), "GiBps_data": round(B * k * S / GIB / (f_ms * 1e-3), 2),
                 "hbm_GBps_algorithmic": round(algo_bytes / (f_ms * 1e-3) / 1e9, 1),
+                "kernel": "encode_crc_tile_kernel + tile_combine_kernel",
+                "persistent_segment_kernel_ms": round(p_ms, 3),
                 "separate_encode_plus_crc_ms": round(launch_ms + crc_ms, 3) if blk else None}
         # PackTracts (§8f row 3): lay tracts of random length (64 KiB..8 MiB, from a 4 GiB
         # device pool) at padToLength-aligned offsets into the B*k data pieces, zero-filling

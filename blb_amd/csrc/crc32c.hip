@@ -367,6 +367,20 @@ std::map<std::pair<int, uint64_t>, CrcConsts*> g_consts;  // device copies, proc
 
 }  // namespace
 
+void crc_shift_matrix(uint64_t n, uint32_t col[32]) {
+    uint32_t t0[256];
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t v = i;
+        for (int j = 0; j < 8; ++j) v = (v & 1u) ? (v >> 1) ^ kCrcPoly : v >> 1;
+        t0[i] = v;
+    }
+    Mat32 p[kPow2];
+    p[0] = shift_one_byte(t0);
+    for (int i = 1; i < kPow2; ++i) p[i] = mat_mul(p[i - 1], p[i - 1]);
+    const Mat32 m = mat_pow(p, n);
+    for (int i = 0; i < 32; ++i) col[i] = m.col[i];
+}
+
 hipError_t crc_consts_for(uint64_t seg, const CrcConsts** out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);

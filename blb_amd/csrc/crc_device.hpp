@@ -29,6 +29,9 @@ struct CrcConsts {
 // r's block j is id r * nblocks + j) folds its raw[id * segs_per_block + s] with S_seg
 // (Horner) and applies the init term.  out[id] = crc32.Checksum(block).
 hipError_t crc_consts_for(uint64_t seg, const CrcConsts** out);
+// Host: the column-major matrix S_n (feed n zero bytes), for kernels' constant tables.
+void crc_shift_matrix(uint64_t n, uint32_t col[32]);
+
 hipError_t crc_combine(const CrcConsts* c, const uint32_t* raw, uint64_t len, uint64_t block, uint64_t seg,
                        uint32_t nblocks, uint32_t segs_per_block, uint64_t total_blocks, uint32_t* out,
                        hipStream_t stream);
@@ -84,6 +87,43 @@ __device__ __forceinline__ uint32_t lookup(const LaneTabs& t, uint32_t x) {
 // raw(c || w) for one dword w: slicing-by-4 (4 perms + 4 LDS reads + 2 XOR).
 __device__ __forceinline__ uint32_t slice4(const LaneTabs& t, uint32_t x) {
     return xor3(lookup<0>(t, x), lookup<1>(t, x), lookup<2>(t, x)) ^ lookup<3>(t, x);
+}
+
+// Coalesced loads and stores, ordered for the CRC: instruction q of a row covers its 1 KiB
+// sub-row q (64 pieces of 16 B), and within it lane (h, j) -- h = lane / (64 / P), P =
+// LC / 16 pieces per lane -- takes piece P*j + h.  Lane L's LC contiguous CRC bytes
+// (pieces P*L .. P*L + P-1) then sit in register q = L / (64 / P) of the P lanes (i, L %
+// (64 / P)): a P x P transpose over (lane group, register) that v_permlane{16,32}_swap do
+// in registers (lane_contiguous below), instead of a round trip through LDS.
+template <int LC>
+__device__ __forceinline__ uint32_t lane_piece(uint32_t lane) {
+    if constexpr (LC == 64) return 16u * (4u * (lane & 15u) + (lane >> 4));
+    else return 16u * (2u * (lane & 31u) + (lane >> 5));
+}
+
+// v[q][0..3] = this lane's piece of sub-row q -> v[i][0..3] = piece i of the lane's own
+// LC-byte chunk.  E[row][q] -> E[q][row] with rows = 16-lane (LC 64) or 32-lane (LC 32)
+// lane groups: permlane32_swap(a, b) swaps a's upper-half lanes with b's lower-half lanes,
+// permlane16_swap(a, b) a's odd 16-lane rows with b's even rows.
+template <int LC>
+__device__ __forceinline__ void lane_contiguous(uint32_t (&v)[LC / 4]) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        if constexpr (LC == 64) {
+            auto s02 = __builtin_amdgcn_permlane32_swap(v[d], v[8 + d], false, false);
+            auto s13 = __builtin_amdgcn_permlane32_swap(v[4 + d], v[12 + d], false, false);
+            auto s01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
+            auto s23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
+            v[d] = s01[0];
+            v[4 + d] = s01[1];
+            v[8 + d] = s23[0];
+            v[12 + d] = s23[1];
+        } else {
+            auto s01 = __builtin_amdgcn_permlane32_swap(v[d], v[4 + d], false, false);
+            v[d] = s01[0];
+            v[4 + d] = s01[1];
+        }
+    }
 }
 
 }  // namespace dev

@@ -1,4 +1,7 @@
 // encode_crc.hip -- fused Reed-Solomon encode + CRC-32C of the parity, one pass over HBM.
+// Persistent segment kernel: launch_encode_crc hands the shapes the tile-grid kernel covers
+// (encode_crc_tile.hip, faster) to it and runs this one for the rest (rows = 5, lengths
+// that are not whole 8 KiB tiles, blocks < 8 KiB, views not 16-byte aligned).
 //
 // On blb's RS path every parity shard the encoder writes is checksummed next: the
 // tractserver ships each parity increment with CtlWrite, whose bulk RPC frame carries a
@@ -72,43 +75,6 @@ struct Geo {
     static constexpr int kQ = LC / 16;             // dwordx4 per lane per row
     static constexpr int kVar = LC == 64 ? 0 : 1;  // CrcConsts gap / wlvl variant
 };
-
-// Coalesced loads and stores, ordered for the CRC: instruction q of a row covers its 1 KiB
-// sub-row q (64 pieces of 16 B), and within it lane (h, j) -- h = lane / (64 / P), P =
-// LC / 16 pieces per lane -- takes piece P*j + h.  Lane L's LC contiguous CRC bytes
-// (pieces P*L .. P*L + P-1) then sit in register q = L / (64 / P) of the P lanes (i, L %
-// (64 / P)): a P x P transpose over (lane group, register) that v_permlane{16,32}_swap do
-// in registers (lane_contiguous below), instead of a round trip through LDS.
-template <int LC>
-__device__ __forceinline__ uint32_t lane_piece(uint32_t lane) {
-    if constexpr (LC == 64) return 16u * (4u * (lane & 15u) + (lane >> 4));
-    else return 16u * (2u * (lane & 31u) + (lane >> 5));
-}
-
-// v[q][0..3] = this lane's piece of sub-row q -> v[i][0..3] = piece i of the lane's own
-// LC-byte chunk.  E[row][q] -> E[q][row] with rows = 16-lane (LC 64) or 32-lane (LC 32)
-// lane groups: permlane32_swap(a, b) swaps a's upper-half lanes with b's lower-half lanes,
-// permlane16_swap(a, b) a's odd 16-lane rows with b's even rows.
-template <int LC>
-__device__ __forceinline__ void lane_contiguous(uint32_t (&v)[LC / 4]) {
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        if constexpr (LC == 64) {
-            auto s02 = __builtin_amdgcn_permlane32_swap(v[d], v[8 + d], false, false);
-            auto s13 = __builtin_amdgcn_permlane32_swap(v[4 + d], v[12 + d], false, false);
-            auto s01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
-            auto s23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
-            v[d] = s01[0];
-            v[4 + d] = s01[1];
-            v[8 + d] = s23[0];
-            v[12 + d] = s23[1];
-        } else {
-            auto s01 = __builtin_amdgcn_permlane32_swap(v[d], v[4 + d], false, false);
-            v[d] = s01[0];
-            v[4 + d] = s01[1];
-        }
-    }
-}
 
 // Loads row r of the segment (plain dwordx4 per 16-byte piece, see lane_piece).
 template <int K, int LC>
@@ -395,6 +361,8 @@ bool encode_crc_supported(const EncodeCrcArgs& a) {
 hipError_t launch_encode_crc(const EncodeCrcArgs& in, hipStream_t stream) {
     if (in.B == 0 || in.S == 0) return hipSuccess;
     if (!encode_crc_supported(in) || !in.crc) return hipErrorInvalidValue;
+    const bool persistent = getenv("BLBRS_EC_PERSISTENT") != nullptr;  // per call: A/B in one process
+    if (!persistent && encode_crc_tile_supported(in)) return launch_encode_crc_tile(in, stream);
     const KernelFn fn = pick(in.k, in.rows);
     const CrcConsts* c = nullptr;
     hipError_t e = crc_consts_for(kSeg, &c);

@@ -25,7 +25,14 @@ struct EncodeCrcArgs {
 // base/strides/length/block.  Otherwise the caller runs the coding pass and crc32c_blocks.
 bool encode_crc_supported(const EncodeCrcArgs& a);
 
-// Launches the fused kernel plus the per-block combine on `stream`.
+// Launches the fused kernel plus the per-block combine on `stream`: the tile-grid kernel
+// (encode_crc_tile.hip) when it covers the shape, else the persistent segment kernel.
+// BLBRS_EC_PERSISTENT=1 forces the segment kernel (A/B measurements).
 hipError_t launch_encode_crc(const EncodeCrcArgs& a, hipStream_t stream);
+
+// The tile-grid form: rows <= 4, 16-byte aligned base and strides, S a multiple of the
+// 8 KiB tile, block >= tile and a multiple of 4.
+bool encode_crc_tile_supported(const EncodeCrcArgs& a);
+hipError_t launch_encode_crc_tile(const EncodeCrcArgs& a, hipStream_t stream);
 
 }  // namespace blbrs
