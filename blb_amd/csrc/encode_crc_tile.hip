@@ -12,9 +12,9 @@
 //    and stored with coalesced 1 KiB instructions (lane_piece) and transposed in registers
 //    (lane_contiguous) so that lane L holds the LC contiguous bytes at tile offset LC * tid.
 //  * CRC: each lane runs one slicing-by-4 chain per parity row over its LC bytes (tables in
-//    LDS, C interleaved copies to spread bank conflicts), shifts it to its wave row's end
-//    with its own matrix S_{LC*(63-lane)} (64 matrices staged in LDS), and the wave XORs its
-//    lanes; one lane per row shifts the 4 row values to the tile end (S_{64*LC*(3-w)}) and
+//    LDS; C interleaved copies would spread bank conflicts but cost more to stage, so C = 1),
+//    shifts it to its wave row's end with its own matrix S_{LC*(63-lane)} (64 matrices
+//    staged in LDS), and the wave XORs its lanes; one lane per row shifts the 4 row values to the tile end (S_{64*LC*(3-w)}) and
 //    XORs them.  Per workgroup that is 4*C + 8 KiB of constants from L2 -- kept small
 //    because every workgroup stages them for one tile.
 //  * Tiles ignore block boundaries.  A tile that contains one (at dword offset o) also runs
@@ -38,7 +38,7 @@ using namespace dev;
 constexpr int kTThreads = 256;                     // 4 waves, one row each
 constexpr uint64_t kOrd = 0x7FFFFFFFull;            // S_{kOrd} = I (checked on the host)
 #ifndef BLBRS_ECT_COPIES
-#define BLBRS_ECT_COPIES 2
+#define BLBRS_ECT_COPIES 1
 #endif
 constexpr int kCopies = BLBRS_ECT_COPIES;           // interleaved copies of the slicing tables
 
