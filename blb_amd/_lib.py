@@ -40,12 +40,50 @@ SIGNATURES = {
     "blbrs_batcher_free": (None, [_P]),
     "blbrs_encoder_set_batcher": (_I, [_P, _P]),
     "blbrs_batcher_stats": (_I, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "blbrs_new_on": (_I, [_I, _I, _P, _I, ctypes.POINTER(_P)]),
+    "blbrs_encoder_devices": (_I, [_P, _P, _I, ctypes.POINTER(_I)]),
+    "blbrs_set_default_devices": (_I, [_P, _I]),
+    "blbrs_encode_parts": (_I, [_P, _P, _SZ, _SZ]),
+    "blbrs_reconstruct_parts": (_I, [_P, _P, _SZ, _SZ, _P, _I]),
+    "blbrs_verify_parts": (_I, [_P, _P, _SZ, _SZ, _P]),
+    "blbrs_batcher_new_on": (_I, [_I, _I, _P, _I, ctypes.POINTER(_P)]),
+    "blbrs_buffer_get": (_I, [_SZ, ctypes.POINTER(_P), ctypes.POINTER(_SZ)]),
+    "blbrs_buffer_put": (_I, [_P]),
+    "blbrs_pool_set_idle_limit": (_I, [_SZ]),
+    "blbrs_get_pool_stats": (_I, [_P]),
+    "blbrs_host_alloc": (_I, [_SZ, ctypes.POINTER(_P)]),
+    "blbrs_host_free": (_I, [_P]),
+    "blbrs_host_register": (_I, [_P, _SZ]),
+    "blbrs_host_unregister": (_I, [_P]),
+    "blbrs_set_worker_limit": (_I, [_I]),
+    "blbrs_get_device_stats": (_I, [_I, _P]),
+    "blbrs_trim": (_I, []),
     "blbrs_set_device": (_I, [_I]),
     "blbrs_device_count": (_I, [ctypes.POINTER(_I)]),
     "blbrs_last_error": (ctypes.c_char_p, []),
     "blbrs_version": (ctypes.c_char_p, []),
     "blbrs_strerror": (ctypes.c_char_p, [_I]),
 }
+
+
+
+class DeviceStats(ctypes.Structure):
+    """blbrs_device_stats"""
+    _fields_ = [("workers", ctypes.c_uint64), ("idle", ctypes.c_uint64), ("waits", ctypes.c_uint64),
+                ("staging_bytes", ctypes.c_uint64), ("calls", ctypes.c_uint64), ("inflight", ctypes.c_int64)]
+
+
+class PoolStats(ctypes.Structure):
+    """blbrs_pool_stats"""
+    _fields_ = [("gets", ctypes.c_uint64), ("puts", ctypes.c_uint64), ("allocs", ctypes.c_uint64),
+                ("frees", ctypes.c_uint64), ("live_bytes", ctypes.c_uint64), ("idle_bytes", ctypes.c_uint64)]
+
+
+class DevPart(ctypes.Structure):
+    """blbrs_dev_part"""
+    _fields_ = [("stripes", _P), ("shard_stride", _SZ), ("stripe_stride", _SZ), ("batch", _SZ),
+                ("stream", _P)]
+
 
 _lib = None
 

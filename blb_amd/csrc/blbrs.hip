@@ -1,17 +1,19 @@
-// blbrs.hip -- host runtime + C ABI (include/blb_rs.h) of the MI355X RS engine.
+// blbrs.hip -- the C ABI (include/blb_rs.h) of the MI355X RS engine.
 //
-// What lives here (the kernels are in rs_kernels.hip):
+// What lives here (the kernels are in rs_kernels.hip, the per-device runtime in runtime.hip):
 //   * reedsolomon.New equivalent: (k+m) x k matrix build (gf256.hpp), argument checks with
-//     klauspost's error values.
+//     klauspost's error values, a device list per encoder.
 //   * Coding plans: for each (operation, erasure pattern) the coefficient rows, their
 //     v_perm lookup tables and shard index lists, uploaded once per device and cached on
 //     the encoder -- the counterpart of klauspost's inversion tree (decode matrices
 //     cached by invalid-index set) but holding device-ready tables.
 //   * Host-memory Encoder methods (Encode / Verify / Reconstruct / ReconstructData) with
-//     klauspost's shard conventions, each call borrowing a per-device stream worker so
-//     concurrent callers (goroutines through cgo) never share a stream.
-//   * Device-resident batched entry points on caller streams, and the pinned-host
-//     streaming encoder (H2D / kernel / D2H overlapped over several streams).
+//     klauspost's shard conventions; each call runs on the least-loaded device of its
+//     encoder on a leased stream worker, so concurrent callers (goroutines through cgo)
+//     never share a stream and never depend on the calling thread's HIP device.
+//   * Device-resident batched entry points (on the device owning the stripes, on caller
+//     streams), multi-device parts, and the host-batch encoder split over the device list.
+//   * The reconstruct batcher (client degraded reads).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,34 +34,20 @@
 #include "../../include/blb_rs.h"
 #include "crc32c.hpp"
 #include "encode_crc.hpp"
-#include "pack.hpp"
 #include "gf256.hpp"
+#include "pack.hpp"
 #include "rs_kernels.hpp"
+#include "runtime.hpp"
 
 using namespace blbrs;
+using rt::aligned16;
+using rt::fail;
+using rt::hip_fail;
+using rt::round_up;
+
+#define HIP_TRY(expr) BLBRS_HIP_TRY(expr)
 
 namespace {
-
-thread_local std::string g_last_error;
-
-int fail(int code, const std::string& msg) {
-    g_last_error = msg;
-    return code;
-}
-
-int hip_fail(hipError_t e, const char* what) {
-    std::string m = std::string(what) + ": " + hipGetErrorString(e);
-    g_last_error = m;
-    return BLBRS_ERR_HIP;
-}
-
-#define HIP_TRY(expr)                                         \
-    do {                                                      \
-        hipError_t e_ = (expr);                               \
-        if (e_ != hipSuccess) return hip_fail(e_, #expr);     \
-    } while (0)
-
-size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---------------------------------------------------------------------------------------
 // Coding plans
@@ -108,15 +96,14 @@ struct DevPlan {
     std::vector<DevPass> passes;
     int device = -1;
     ~DevPlan() {
-        int cur = 0;
-        if (hipGetDevice(&cur) != hipSuccess) return;
-        if (hipSetDevice(device) != hipSuccess) return;
+        rt::DeviceGuard g;
+        if (g.enter(device) != BLBRS_OK) return;
         for (auto& p : passes)
             if (p.mem) (void)hipFree(p.mem);
-        (void)hipSetDevice(cur);
     }
 };
 
+// Uploads on the current device (== device).
 int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
     auto dp = std::make_unique<DevPlan>();
     dp->device = device;
@@ -143,6 +130,15 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
     return BLBRS_OK;
 }
 
+std::string plan_key(bool encode, const std::vector<uint8_t>& present, bool data_only) {
+    if (encode) return "E";
+    std::string key(present.size() + 2, '0');
+    key[0] = 'R';
+    key[1] = data_only ? 'd' : 'a';
+    for (size_t i = 0; i < present.size(); ++i) key[i + 2] = present[i] ? '1' : '0';
+    return key;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
@@ -151,7 +147,7 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
 
 // Matrix and plan caches of one (k, m).  Shared by every blbrs_encoder handle with that
 // shape: blb makes a fresh reedsolomon.New(n, m) per client reconstruct
-// (client/blb/reconstruct.go:172), and a shared core keeps those calls from rebuilding
+// (client/blb/reconstruct.go:166), and a shared core keeps those calls from rebuilding
 // and re-uploading plans -- and lets a batcher merge them.
 struct EncoderCore {
     int k = 0, m = 0;
@@ -181,10 +177,7 @@ struct EncoderCore {
     // (unless data_only) P[j] * inv(M[valid]) for missing parity j -- one pass produces
     // every missing shard straight from the k survivors.  Returns nullptr + rc on error.
     std::shared_ptr<HostPlan> decode_plan(const std::vector<uint8_t>& present, bool data_only, int* rc) {
-        std::string key(present.size() + 2, '0');
-        key[0] = 'R';
-        key[1] = data_only ? 'd' : 'a';
-        for (size_t i = 0; i < present.size(); ++i) key[i + 2] = present[i] ? '1' : '0';
+        const std::string key = plan_key(false, present, data_only);
         std::lock_guard<std::mutex> g(mu);
         auto& slot = host_plans[key];
         if (slot) return slot;
@@ -221,7 +214,8 @@ struct EncoderCore {
         return slot;
     }
 
-    // Device tables for `hp` on `device` (uploaded on first use).
+    // Device tables for `hp` on `device` (uploaded on first use; the caller has made
+    // `device` current).
     int dev_plan(const std::string& key, const HostPlan& hp, int device, const DevPlan** out) {
         std::lock_guard<std::mutex> g(mu);
         auto& slot = dev_plans[{device, key}];
@@ -241,12 +235,28 @@ struct blbrs_encoder {
     std::shared_ptr<EncoderCore> core;
     int k = 0, m = 0;
     std::atomic<blbrs_batcher*> batcher{nullptr};  // routes host Reconstruct[Data] (blbrs_encoder_set_batcher)
+    std::mutex dev_mu;
+    std::vector<int> devices;   // explicit list, or empty until the default list is resolved
+    bool resolved = false;
+    std::atomic<unsigned> rr{0};
+
     std::shared_ptr<HostPlan> encode_plan() { return core->encode_plan(); }
     std::shared_ptr<HostPlan> decode_plan(const std::vector<uint8_t>& present, bool data_only, int* rc) {
         return core->decode_plan(present, data_only, rc);
     }
     int dev_plan(const std::string& key, const HostPlan& hp, int device, const DevPlan** out) {
         return core->dev_plan(key, hp, device, out);
+    }
+    // The device list: explicit (checked once) or the process default (resolved once).
+    int lanes(std::vector<int>* out) {
+        std::lock_guard<std::mutex> g(dev_mu);
+        if (!resolved) {
+            int rc = devices.empty() ? rt::default_devices(&devices) : rt::check_devices(devices);
+            if (rc) return rc;
+            resolved = true;
+        }
+        *out = devices;
+        return BLBRS_OK;
     }
 };
 
@@ -266,15 +276,6 @@ std::shared_ptr<EncoderCore> core_for(int k, int m) {
     if (!build_matrix(k, m, c->matrix)) return nullptr;
     w = c;
     return c;
-}
-
-std::string plan_key(bool encode, const std::vector<uint8_t>& present, bool data_only) {
-    if (encode) return "E";
-    std::string key(present.size() + 2, '0');
-    key[0] = 'R';
-    key[1] = data_only ? 'd' : 'a';
-    for (size_t i = 0; i < present.size(); ++i) key[i + 2] = present[i] ? '1' : '0';
-    return key;
 }
 
 // Addressing of one batch of stripes on the device.
@@ -313,94 +314,6 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
     return BLBRS_OK;
 }
 
-// ---- per-device resources ----
-
-// Stream worker for host-memory calls: its own streams and device staging buffer.
-struct Worker {
-    hipStream_t s[2] = {nullptr, nullptr};
-    uint8_t* dbuf = nullptr;
-    size_t cap = 0;
-    int32_t* dflag = nullptr;
-    int device = -1;
-    int ensure(size_t bytes) {
-        if (bytes <= cap) return BLBRS_OK;
-        if (dbuf) (void)hipFree(dbuf);
-        dbuf = nullptr;
-        cap = 0;
-        HIP_TRY(hipMalloc(&dbuf, bytes));
-        cap = bytes;
-        return BLBRS_OK;
-    }
-};
-
-// Pinned + device slot for uploading pointer tables of the *_ptrs entry points.
-struct PtrSlot {
-    std::mutex mu;
-    uint64_t* host = nullptr;
-    uint64_t* dev = nullptr;
-    size_t cap = 0;  // entries
-    hipEvent_t done = nullptr;
-};
-
-struct Device {
-    std::mutex mu;
-    std::vector<Worker*> idle;
-    static constexpr int kSlots = 8;
-    PtrSlot slots[kSlots];
-    std::atomic<unsigned> next_slot{0};
-};
-
-std::mutex g_dev_mu;
-std::map<int, Device*> g_devices;  // never freed (process lifetime)
-
-Device& device_ctx(int dev) {
-    std::lock_guard<std::mutex> g(g_dev_mu);
-    auto& d = g_devices[dev];
-    if (!d) d = new Device();
-    return *d;
-}
-
-int current_device(int* dev) {
-    int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
-    if (e != hipSuccess || n <= 0) return fail(BLBRS_ERR_NO_DEVICE, "no HIP device visible");
-    HIP_TRY(hipGetDevice(dev));
-    return BLBRS_OK;
-}
-
-struct WorkerLease {
-    Device* d = nullptr;
-    Worker* w = nullptr;
-    ~WorkerLease() {
-        if (w) {
-            std::lock_guard<std::mutex> g(d->mu);
-            d->idle.push_back(w);
-        }
-    }
-};
-
-int lease_worker(WorkerLease& lease) {
-    int dev = 0;
-    int rc = current_device(&dev);
-    if (rc) return rc;
-    Device& d = device_ctx(dev);
-    lease.d = &d;
-    {
-        std::lock_guard<std::mutex> g(d.mu);
-        if (!d.idle.empty()) {
-            lease.w = d.idle.back();
-            d.idle.pop_back();
-            return BLBRS_OK;
-        }
-    }
-    auto* w = new Worker();
-    w->device = dev;
-    for (auto& s : w->s) HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    HIP_TRY(hipMalloc(&w->dflag, sizeof(int32_t)));
-    lease.w = w;
-    return BLBRS_OK;
-}
-
 // klauspost checkShards / shardSize.
 int check_shards(int n, const size_t* lens, bool nilok, size_t* size) {
     size_t s = 0;
@@ -413,89 +326,20 @@ int check_shards(int n, const size_t* lens, bool nilok, size_t* size) {
     return BLBRS_OK;
 }
 
-bool aligned16(uintptr_t x) { return (x & 15u) == 0; }
-
-// Upload a host array of device pointers to a device pointer table on `stream`.  The
-// slot's event keeps it busy until the kernels that read it have run.
-struct PtrLease {
-    PtrSlot* slot = nullptr;
-    hipStream_t stream = nullptr;
-    ~PtrLease() {
-        if (slot) {
-            (void)hipEventRecord(slot->done, stream);
-            slot->mu.unlock();
-        }
-    }
-};
-
-int upload_table(const uint64_t* ptrs, size_t count, hipStream_t stream, PtrLease& lease,
-                 const uint64_t** dev_out, bool* aligned) {
-    int dev = 0;
-    int rc = current_device(&dev);
+// The device a device-resident call runs on: the owner of `p` when it is device memory,
+// else the calling thread's current device (pinned host memory is mapped on every device).
+int device_of(const void* p, int* dev) {
+    int n = 0;
+    int rc = rt::device_count(&n);
     if (rc) return rc;
-    Device& d = device_ctx(dev);
-    PtrSlot& s = d.slots[d.next_slot.fetch_add(1) % Device::kSlots];
-    s.mu.lock();
-    if (!s.done) {
-        hipError_t e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
-        if (e != hipSuccess) { s.mu.unlock(); return hip_fail(e, "hipEventCreate"); }
-    } else {
-        hipError_t e = hipEventSynchronize(s.done);
-        if (e != hipSuccess) { s.mu.unlock(); return hip_fail(e, "hipEventSynchronize"); }
+    uint64_t view = 0;
+    int owner = -1;
+    if (p && rt::device_view(p, &view, &owner) && owner >= 0) {
+        *dev = owner;
+        return BLBRS_OK;
     }
-    if (s.cap < count) {
-        if (s.host) (void)hipHostFree(s.host);
-        if (s.dev) (void)hipFree(s.dev);
-        s.host = nullptr;
-        s.dev = nullptr;
-        s.cap = 0;
-        const size_t cap = std::max<size_t>(count, 1024);
-        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&s.host), cap * 8, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.dev), cap * 8);
-        if (e != hipSuccess) { s.mu.unlock(); return hip_fail(e, "ptr table alloc"); }
-        s.cap = cap;
-    }
-    bool al = true;
-    for (size_t i = 0; i < count; ++i) {
-        s.host[i] = ptrs[i];
-        al = al && aligned16(s.host[i]);
-    }
-    lease.slot = &s;
-    lease.stream = stream;
-    HIP_TRY(hipMemcpyAsync(s.dev, s.host, count * 8, hipMemcpyHostToDevice, stream));
-    *dev_out = s.dev;
-    *aligned = al;
+    HIP_TRY(hipGetDevice(dev));
     return BLBRS_OK;
-}
-
-int upload_ptrs(uint8_t* const* ptrs, size_t count, hipStream_t stream, PtrLease& lease,
-                const uint64_t** dev_out, bool* aligned) {
-    std::vector<uint64_t> v(count);
-    for (size_t i = 0; i < count; ++i) {
-        if (!ptrs[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
-        v[i] = reinterpret_cast<uint64_t>(ptrs[i]);
-    }
-    return upload_table(v.data(), count, stream, lease, dev_out, aligned);
-}
-
-// Address under which the GPU can access `p`: device memory as is, pinned host memory
-// (hipHostMalloc / hipHostRegister) through its device mapping.  False for pageable memory.
-bool device_view(const void* p, uint64_t* out) {
-    hipPointerAttribute_t attr;
-    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-        (void)hipGetLastError();  // pageable memory: clear the sticky error
-        return false;
-    }
-    if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) {
-        *out = reinterpret_cast<uint64_t>(p);
-        return true;
-    }
-    if (attr.type == hipMemoryTypeHost && attr.devicePointer && attr.hostPointer) {
-        *out = reinterpret_cast<uint64_t>(attr.devicePointer) +
-               (reinterpret_cast<uintptr_t>(p) - reinterpret_cast<uintptr_t>(attr.hostPointer));
-        return true;
-    }
-    return false;
 }
 
 // One step of a host-memory call: a plan run in store or verify mode.
@@ -505,21 +349,23 @@ struct Step {
     Mode mode;
 };
 
-// Host-memory coding.  Steps run in order over the same stripe, so a later step sees what
-// an earlier one wrote (Reconstruct then Verify = reconstructAndVerify, store.go:1132-1142,
-// in one device round trip).  Shards read by a step and not produced by an earlier step
-// are copied in once; shards written by store steps are copied out.
-int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const* shards, size_t S, int* ok) {
-    WorkerLease lease;
-    int rc = lease_worker(lease);
+// Host-memory coding of `batch` stripes (shards = batch x n pointers, stripe-major) on
+// device `dev` (already current).  Steps run in order over each stripe, so a later step
+// sees what an earlier one wrote (Reconstruct then Verify = reconstructAndVerify,
+// store.go:1132-1142, in one device round trip).  Shards read by a step and not produced by
+// an earlier step are copied in once; shards written by store steps are copied out.
+int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const* shards, size_t batch, size_t S,
+             int* ok, int dev) {
+    rt::WorkerLease w;
+    int rc = w.acquire(dev);
     if (rc) return rc;
-    Worker& w = *lease.w;
+    rt::note_call(dev);
     const int n = enc->k + enc->m;
     std::vector<const DevPlan*> plans(steps.size(), nullptr);
     std::vector<char> produced(n, 0), need_in(n, 0), is_out(n, 0), touched(n, 0);
     bool verify = false;
     for (size_t t = 0; t < steps.size(); ++t) {
-        if ((rc = enc->dev_plan(steps[t].key, *steps[t].hp, w.device, &plans[t]))) return rc;
+        if ((rc = enc->dev_plan(steps[t].key, *steps[t].hp, dev, &plans[t]))) return rc;
         const HostPlan& hp = *steps[t].hp;
         for (int32_t i : hp.in_idx) {
             touched[i] = 1;
@@ -538,78 +384,114 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     }
     // Zero-copy: when every shard the steps touch is pinned (or device) memory, the kernels
     // read and write it in place over PCIe -- no staging, and both link directions busy at
-    // once (RS(6,3): 50.8 GiB/s of data vs 37.3 through copy engines; profiles/r01/zc.txt).
+    // once (RS(6,3): 50.8 GiB/s of data vs 37.3 through copy engines).
     {
-        std::vector<uint64_t> view(n, 0);
+        std::vector<uint64_t> view(batch * n, 0);
         bool all = true;
-        for (int i = 0; i < n && all; ++i)
-            if (touched[i]) all = device_view(shards[i], &view[i]);
+        for (size_t b = 0; b < batch && all; ++b)
+            for (int i = 0; i < n && all; ++i)
+                if (touched[i]) all = rt::device_view(shards[b * n + i], &view[b * n + i]);
         if (all) {
-            PtrLease pl;
             Stripes st;
             st.nshards = n;
-            if ((rc = upload_table(view.data(), n, w.s[0], pl, &st.ptrs, &st.aligned))) return rc;
-            if (verify) HIP_TRY(hipMemsetAsync(w.dflag, 0, sizeof(int32_t), w.s[0]));
+            if ((rc = w->upload_table(view.data(), view.size(), &st.ptrs, &st.aligned))) return rc;
+            if (verify) HIP_TRY(hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]));
             for (size_t t = 0; t < steps.size(); ++t)
-                if ((rc = run_plan(*plans[t], st, 1, S, steps[t].mode, w.dflag, w.s[0]))) return rc;
+                if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) {
+                    (void)hipStreamSynchronize(w->s[0]);
+                    return rc;
+                }
             int32_t flag = 0;
-            if (verify) HIP_TRY(hipMemcpyAsync(&flag, w.dflag, sizeof(int32_t), hipMemcpyDeviceToHost, w.s[0]));
-            HIP_TRY(hipStreamSynchronize(w.s[0]));
+            if (verify) HIP_TRY(hipMemcpyAsync(&flag, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]));
+            HIP_TRY(hipStreamSynchronize(w->s[0]));
             if (ok) *ok = flag ? 0 : 1;
             return BLBRS_OK;
         }
     }
-    // Staged: 1 MiB column chunks alternate over the worker's two streams, so the H2D of
-    // chunk j+1 overlaps the kernels and D2H of chunk j.
-    const size_t Sp = round_up(S, 256);  // padded shard stride keeps every shard 16B-aligned
-    if ((rc = w.ensure(static_cast<size_t>(n) * Sp))) return rc;
-    const size_t chunk = S <= (size_t{2} << 20) ? S : (size_t{1} << 20);
+    // Staged: column chunks of each stripe alternate over the worker's two streams and two
+    // ring slots, so the H2D of unit u+1 overlaps the kernels and D2H of unit u.  A slot is
+    // reused two units later on the same stream, i.e. after that unit's D2H -- in stream
+    // order, no event needed.  Device staging is bounded by 2 x kStageSlotBudget.
+    const size_t Sp = round_up(S, 256);
+    size_t chunk = S;
+    if (S > (size_t{2} << 20) || static_cast<size_t>(n) * Sp > rt::kStageSlotBudget)
+        chunk = std::max<size_t>(4096, std::min<size_t>(size_t{1} << 20, rt::kStageSlotBudget / n / 256 * 256));
+    const size_t cp = round_up(chunk, 256);
+    const size_t slot_bytes = static_cast<size_t>(n) * cp;
+    if ((rc = w->ensure_stage(2 * slot_bytes))) return rc;
     hipEvent_t ev = nullptr;
+    struct EvFree {
+        hipEvent_t& e;
+        ~EvFree() {
+            if (e) (void)hipEventDestroy(e);
+        }
+    } ev_free{ev};
+    auto drain = [&](int rc_) {
+        (void)hipStreamSynchronize(w->s[0]);
+        (void)hipStreamSynchronize(w->s[1]);
+        return rc_;
+    };
     if (verify) {
-        HIP_TRY(hipMemsetAsync(w.dflag, 0, sizeof(int32_t), w.s[0]));
+        HIP_TRY(hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]));
         HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(ev, w.s[0]));
-        HIP_TRY(hipStreamWaitEvent(w.s[1], ev, 0));
+        HIP_TRY(hipEventRecord(ev, w->s[0]));
+        HIP_TRY(hipStreamWaitEvent(w->s[1], ev, 0));
     }
-    int j = 0;
-    for (size_t off = 0; off < S; off += chunk, ++j) {
-        const size_t len = std::min(chunk, S - off);
-        hipStream_t s = w.s[j & 1];
-        for (int i = 0; i < n; ++i)
-            if (need_in[i])
-                HIP_TRY(hipMemcpyAsync(w.dbuf + static_cast<size_t>(i) * Sp + off, shards[i] + off, len,
-                                       hipMemcpyHostToDevice, s));
-        Stripes st;
-        st.base = w.dbuf + off;
-        st.shard_stride = Sp;
-        st.stripe_stride = static_cast<uint64_t>(n) * Sp;
-        st.aligned = aligned16(off);
-        for (size_t t = 0; t < steps.size(); ++t)
-            if ((rc = run_plan(*plans[t], st, 1, len, steps[t].mode, w.dflag, s))) return rc;
-        for (int i = 0; i < n; ++i)
-            if (is_out[i])
-                HIP_TRY(hipMemcpyAsync(shards[i] + off, w.dbuf + static_cast<size_t>(i) * Sp + off, len,
-                                       hipMemcpyDeviceToHost, s));
+    size_t u = 0;
+    for (size_t b = 0; b < batch; ++b) {
+        uint8_t* const* sh = shards + b * n;
+        for (size_t off = 0; off < S; off += chunk, ++u) {
+            const size_t len = std::min(chunk, S - off);
+            hipStream_t s = w->s[u & 1];
+            uint8_t* slot = w->stage + (u & 1) * slot_bytes;
+            hipError_t e = hipSuccess;
+            for (int i = 0; i < n && e == hipSuccess; ++i)
+                if (need_in[i]) e = hipMemcpyAsync(slot + i * cp, sh[i] + off, len, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) return drain(hip_fail(e, "H2D"));
+            Stripes st;
+            st.base = slot;
+            st.shard_stride = cp;
+            st.stripe_stride = slot_bytes;
+            st.aligned = true;
+            for (size_t t = 0; t < steps.size(); ++t)
+                if ((rc = run_plan(*plans[t], st, 1, len, steps[t].mode, w->flag, s))) return drain(rc);
+            for (int i = 0; i < n && e == hipSuccess; ++i)
+                if (is_out[i]) e = hipMemcpyAsync(sh[i] + off, slot + i * cp, len, hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) return drain(hip_fail(e, "D2H"));
+        }
     }
     int32_t flag = 0;
     if (verify) {
-        HIP_TRY(hipEventRecord(ev, w.s[1]));
-        HIP_TRY(hipStreamWaitEvent(w.s[0], ev, 0));
-        HIP_TRY(hipMemcpyAsync(&flag, w.dflag, sizeof(int32_t), hipMemcpyDeviceToHost, w.s[0]));
+        HIP_TRY(hipEventRecord(ev, w->s[1]));
+        HIP_TRY(hipStreamWaitEvent(w->s[0], ev, 0));
+        HIP_TRY(hipMemcpyAsync(&flag, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]));
     }
-    HIP_TRY(hipStreamSynchronize(w.s[0]));
-    HIP_TRY(hipStreamSynchronize(w.s[1]));
-    if (ev) (void)hipEventDestroy(ev);
+    HIP_TRY(hipStreamSynchronize(w->s[0]));
+    HIP_TRY(hipStreamSynchronize(w->s[1]));
     if (ok) *ok = flag ? 0 : 1;
     return BLBRS_OK;
 }
 
-int host_code(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, uint8_t* const* shards,
-              size_t S, Mode mode, int* ok) {
-    return host_run(enc, {Step{key, &hp, mode}}, shards, S, ok);
+// A host-memory call: pick the device (the owner of any device-memory shard, else the
+// least-loaded entry of the encoder's list), make it current for the call and run.
+int host_call(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const* shards, size_t S, int* ok) {
+    std::vector<int> lanes;
+    int rc = enc->lanes(&lanes);
+    if (rc) return rc;
+    const int n = enc->k + enc->m;
+    int dev = -1;
+    for (int i = 0; i < n && dev < 0; ++i) {
+        uint64_t view = 0;
+        int owner = -1;
+        if (shards[i] && rt::device_view(shards[i], &view, &owner) && owner >= 0) dev = owner;
+    }
+    if (dev < 0) dev = lanes[rt::pick_lane(lanes, enc->rr)];
+    rt::LoadTicket ticket;
+    ticket.take(dev);
+    rt::DeviceGuard guard;
+    if ((rc = guard.enter(dev))) return rc;
+    return host_run(enc, steps, shards, 1, S, ok, dev);
 }
-
-int current_dev_or_fail(int* dev) { return current_device(dev); }
 
 std::vector<uint8_t> present_vec(const blbrs_encoder* enc, const uint8_t* present) {
     std::vector<uint8_t> p(enc->k + enc->m);
@@ -623,102 +505,166 @@ std::vector<uint8_t> present_vec(const blbrs_encoder* enc, const uint8_t* presen
 // stripe of `length`-byte pieces; MaxInFlight (:19,35-45) lets many run at once.  Alone,
 // each call is a launch plus a stream round trip for a few KiB..MiB of work.  A batcher
 // collects the calls that arrive within `window_us` (or until `max_batch` are waiting) and
-// runs them as ONE launch per (encoder, erasure pattern, length) group over a device
-// pointer table, with one stream sync for the whole batch.  Shards in pinned or device
-// memory are used in place; pageable shards are staged by the CALLING thread through its
-// own pinned buffer, so the memcpys of concurrent callers run in parallel.
+// runs them as ONE launch per (shape, erasure pattern, length) group over a device pointer
+// table, with one stream sync for the whole batch.  Each device has a queue drained by two
+// lanes (own stream and table each): while one lane's batch runs and syncs, the other
+// collects the next -- the batches pipeline.  Shards in pinned or device memory are used in
+// place; pageable shards are staged by the CALLING thread through a pooled pinned buffer.
 struct BatchReq {
-    blbrs_encoder* enc = nullptr;
+    EncoderCore* core = nullptr;
     std::shared_ptr<HostPlan> hp;
     std::string key;
     std::vector<uint64_t> views;  // device-visible address per shard slot (0 = unused)
     size_t S = 0;
+    int dev = -1;                 // device that must run it (device-memory shards), -1 = any
     std::chrono::steady_clock::time_point arrival;
     int rc = BLBRS_OK;
+    std::string msg;              // error text, re-raised on the caller's thread
     bool done = false;
-};
-
-// Per-thread pinned staging for pageable shards.
-struct PinnedStage {
-    uint8_t* p = nullptr;
-    size_t cap = 0;
-    ~PinnedStage() {
-        if (p) (void)hipHostFree(p);
-    }
-    int ensure(size_t bytes) {
-        if (bytes <= cap) return BLBRS_OK;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p), bytes, hipHostMallocDefault));
-        cap = bytes;
-        return BLBRS_OK;
-    }
 };
 
 }  // namespace
 
 struct blbrs_batcher {
-    int device = 0;
+    struct Queue {
+        std::deque<BatchReq*> q;
+        std::condition_variable cv;
+    };
+    struct Lane {
+        int device = 0;
+        hipStream_t stream = nullptr;
+        uint64_t* tab_host = nullptr;
+        uint64_t* tab_dev = nullptr;
+        size_t tab_cap = 0;
+        std::thread th;
+    };
     size_t max_batch = 64;
     std::chrono::microseconds window{200};
-    hipStream_t stream = nullptr;
+    std::vector<int> devices;  // distinct devices
     std::mutex mu;
-    std::condition_variable cv_in, cv_done;
-    std::deque<BatchReq*> q;
+    std::condition_variable cv_done;
+    std::map<int, Queue> queues;
+    std::vector<std::unique_ptr<Lane>> lanes;
+    std::atomic<unsigned> rr{0};
     bool stop = false;
-    std::thread th;
     std::atomic<uint64_t> launches{0}, requests{0};
 
-    void run() {
-        (void)hipSetDevice(device);
+    void run(Lane* lane) {
+        rt::DeviceGuard guard;
+        if (guard.enter(lane->device) != BLBRS_OK) return;
+        Queue& qu = queues[lane->device];
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
-            cv_in.wait(lk, [&] { return stop || !q.empty(); });
-            if (q.empty()) return;  // stop requested and nothing left
-            const auto deadline = q.front()->arrival + window;
-            cv_in.wait_until(lk, deadline, [&] { return stop || q.size() >= max_batch; });
+            qu.cv.wait(lk, [&] { return stop || !qu.q.empty(); });
+            if (qu.q.empty()) return;  // stop requested and nothing left
+            const auto deadline = qu.q.front()->arrival + window;
+            qu.cv.wait_until(lk, deadline, [&] { return stop || qu.q.size() >= max_batch; });
+            if (qu.q.empty()) continue;  // the other lane took them
             std::vector<BatchReq*> batch;
-            while (!q.empty() && batch.size() < max_batch) {
-                batch.push_back(q.front());
-                q.pop_front();
+            while (!qu.q.empty() && batch.size() < max_batch) {
+                batch.push_back(qu.q.front());
+                qu.q.pop_front();
             }
+            if (!qu.q.empty()) qu.cv.notify_one();
             lk.unlock();
-            process(batch);
+            process(lane, batch);
             lk.lock();
             for (BatchReq* r : batch) r->done = true;
             cv_done.notify_all();
         }
     }
 
-    void process(std::vector<BatchReq*>& batch) {
-        // Handles of one (k, m) share a core, so calls from different encoders merge.
+    int upload(Lane* lane, const std::vector<uint64_t>& table, const uint64_t** dev_out, bool* aligned) {
+        if (table.size() > lane->tab_cap) {
+            if (lane->tab_host) (void)hipHostFree(lane->tab_host);
+            if (lane->tab_dev) (void)hipFree(lane->tab_dev);
+            lane->tab_host = nullptr;
+            lane->tab_dev = nullptr;
+            lane->tab_cap = 0;
+            const size_t cap = std::max<size_t>(table.size(), 1024);
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&lane->tab_host), cap * 8, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&lane->tab_dev), cap * 8));
+            lane->tab_cap = cap;
+        }
+        bool al = true;
+        for (size_t i = 0; i < table.size(); ++i) {
+            lane->tab_host[i] = table[i];
+            al = al && aligned16(table[i]);
+        }
+        HIP_TRY(hipMemcpyAsync(lane->tab_dev, lane->tab_host, table.size() * 8, hipMemcpyHostToDevice, lane->stream));
+        *dev_out = lane->tab_dev;
+        *aligned = al;
+        return BLBRS_OK;
+    }
+
+    void process(Lane* lane, std::vector<BatchReq*>& batch) {
+        // Handles of one (k, m) share a core, so calls from different encoders merge.  The
+        // groups share the lane's table, so they run one after the other.
         std::map<std::tuple<EncoderCore*, std::string, size_t>, std::vector<BatchReq*>> groups;
-        for (BatchReq* r : batch) groups[{r->enc->core.get(), r->key, r->S}].push_back(r);
+        for (BatchReq* r : batch) groups[{r->core, r->key, r->S}].push_back(r);
+        rt::LoadTicket ticket;
+        ticket.take(lane->device);
         for (auto& [gk, reqs] : groups) {
-            EncoderCore* enc = std::get<0>(gk);
-            const size_t S = std::get<2>(gk), n = static_cast<size_t>(enc->k + enc->m);
+            EncoderCore* core = std::get<0>(gk);
+            const size_t S = std::get<2>(gk), n = static_cast<size_t>(core->k + core->m);
             const DevPlan* plan = nullptr;
-            int rc = enc->dev_plan(std::get<1>(gk), *reqs[0]->hp, device, &plan);
+            int rc = core->dev_plan(std::get<1>(gk), *reqs[0]->hp, lane->device, &plan);
             if (rc == BLBRS_OK) {
                 std::vector<uint64_t> table(reqs.size() * n);
                 for (size_t j = 0; j < reqs.size(); ++j)
                     std::copy(reqs[j]->views.begin(), reqs[j]->views.end(), table.begin() + j * n);
-                PtrLease pl;
                 Stripes st;
                 st.nshards = static_cast<uint32_t>(n);
-                rc = upload_table(table.data(), table.size(), stream, pl, &st.ptrs, &st.aligned);
-                if (rc == BLBRS_OK) rc = run_plan(*plan, st, reqs.size(), S, Mode::kStore, nullptr, stream);
+                rc = upload(lane, table, &st.ptrs, &st.aligned);
+                if (rc == BLBRS_OK) rc = run_plan(*plan, st, reqs.size(), S, Mode::kStore, nullptr, lane->stream);
                 if (rc == BLBRS_OK) launches.fetch_add(1);
+                // The table is rewritten by the next group: wait for this one's launch.
+                const hipError_t e = hipStreamSynchronize(lane->stream);
+                if (rc == BLBRS_OK && e != hipSuccess) rc = hip_fail(e, "batched reconstruct");
             }
-            for (BatchReq* r : reqs) r->rc = rc;
-        }
-        const hipError_t e = hipStreamSynchronize(stream);
-        if (e != hipSuccess) {
-            const int rc = hip_fail(e, "batched reconstruct");
-            for (BatchReq* r : batch) r->rc = rc;
+            for (BatchReq* r : reqs) {
+                r->rc = rc;
+                if (rc != BLBRS_OK) r->msg = rt::last_error();
+            }
         }
         requests.fetch_add(batch.size());
+    }
+
+    // Queue `r` (mu held): on its required device, else the device with the shortest queue.
+    void enqueue(BatchReq* r) {
+        int dev = r->dev;
+        if (dev < 0 || !queues.count(dev)) {
+            const size_t start = rr.fetch_add(1) % devices.size();
+            dev = devices[start];
+            size_t best = queues[dev].q.size();
+            for (size_t j = 1; j < devices.size(); ++j) {
+                const int d = devices[(start + j) % devices.size()];
+                if (queues[d].q.size() < best) {
+                    best = queues[d].q.size();
+                    dev = d;
+                }
+            }
+        }
+        Queue& qu = queues[dev];
+        qu.q.push_back(r);
+        if (qu.q.size() == 1 || qu.q.size() >= max_batch) qu.cv.notify_one();
+    }
+
+    void shutdown() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            for (auto& [d, qu] : queues) qu.cv.notify_all();
+        }
+        for (auto& l : lanes)
+            if (l->th.joinable()) l->th.join();  // drains the queues first
+        for (auto& l : lanes) {
+            rt::DeviceGuard guard;
+            if (guard.enter(l->device) != BLBRS_OK) continue;
+            if (l->stream) (void)hipStreamDestroy(l->stream);
+            if (l->tab_host) (void)hipHostFree(l->tab_host);
+            if (l->tab_dev) (void)hipFree(l->tab_dev);
+        }
     }
 };
 
@@ -728,10 +674,9 @@ namespace {
 // the decode plan with at least one output; argument checks have been done.
 int batched_reconstruct(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key,
                         std::shared_ptr<HostPlan> hp, uint8_t* const* shards, size_t S) {
-    static thread_local PinnedStage stage;
     const int n = enc->k + enc->m;
     BatchReq req;
-    req.enc = enc;
+    req.core = enc->core.get();
     req.hp = hp;
     req.key = key;
     req.S = S;
@@ -745,32 +690,87 @@ int batched_reconstruct(blbrs_batcher* b, blbrs_encoder* enc, const std::string&
     std::vector<int> slot(n, -1);
     for (auto [i, in] : touched) {
         (void)in;
-        if (!device_view(shards[i], &req.views[i])) slot[i] = static_cast<int>(nstaged++);
+        int owner = -1;
+        if (!rt::device_view(shards[i], &req.views[i], &owner)) {
+            slot[i] = static_cast<int>(nstaged++);
+        } else if (owner >= 0) {
+            if (req.dev >= 0 && req.dev != owner)
+                return fail(BLBRS_ERR_INVALID_ARG, "shards on different devices");
+            req.dev = owner;
+        }
     }
+    struct Staging {
+        uint8_t* p = nullptr;
+        ~Staging() {
+            if (p) (void)rt::pool_put(p);
+        }
+    } stage;
     if (nstaged) {
-        int rc = stage.ensure(nstaged * Sp);
+        size_t cap = 0;
+        int rc = rt::pool_get(nstaged * Sp, &stage.p, &cap);
         if (rc) return rc;
         for (auto [i, in] : touched) {
             if (slot[i] < 0) continue;
             uint8_t* p = stage.p + static_cast<size_t>(slot[i]) * Sp;
             if (in) std::memcpy(p, shards[i], S);
-            if (!device_view(p, &req.views[i])) return fail(BLBRS_ERR_HIP, "pinned staging has no device mapping");
+            if (!rt::device_view(p, &req.views[i])) return fail(BLBRS_ERR_HIP, "pinned staging has no device mapping");
         }
     }
     req.arrival = std::chrono::steady_clock::now();
     {
         std::unique_lock<std::mutex> lk(b->mu);
         if (b->stop) return fail(BLBRS_ERR_INVALID_ARG, "batcher is shutting down");
-        b->q.push_back(&req);
-        if (b->q.size() >= b->max_batch) b->cv_in.notify_one();
-        else if (b->q.size() == 1) b->cv_in.notify_one();
+        b->enqueue(&req);
         b->cv_done.wait(lk, [&] { return req.done; });
     }
-    if (req.rc != BLBRS_OK) return req.rc;
+    if (req.rc != BLBRS_OK) return fail(req.rc, req.msg);
     for (int32_t i : hp->out_idx)
         if (slot[i] >= 0) std::memcpy(shards[i], stage.p + static_cast<size_t>(slot[i]) * Sp, S);
     return BLBRS_OK;
 }
+
+int make_batcher(int max_batch, int window_us, std::vector<int> devs, blbrs_batcher** out) {
+    std::sort(devs.begin(), devs.end());
+    devs.erase(std::unique(devs.begin(), devs.end()), devs.end());
+    auto* b = new blbrs_batcher();
+    b->max_batch = static_cast<size_t>(max_batch);
+    b->window = std::chrono::microseconds(window_us);
+    b->devices = devs;
+    for (int d : devs) {
+        b->queues[d];
+        for (int j = 0; j < 2; ++j) {
+            auto lane = std::make_unique<blbrs_batcher::Lane>();
+            lane->device = d;
+            rt::DeviceGuard guard;
+            int rc = guard.enter(d);
+            hipError_t e = hipSuccess;
+            if (rc == BLBRS_OK) e = hipStreamCreateWithFlags(&lane->stream, hipStreamNonBlocking);
+            if (rc != BLBRS_OK || e != hipSuccess) {
+                b->shutdown();
+                delete b;
+                return rc ? rc : hip_fail(e, "hipStreamCreate");
+            }
+            b->lanes.push_back(std::move(lane));
+        }
+    }
+    for (auto& l : b->lanes) {
+        blbrs_batcher::Lane* lp = l.get();
+        l->th = std::thread([b, lp] { b->run(lp); });
+    }
+    *out = b;
+    return BLBRS_OK;
+}
+
+// Device-resident calls: the stripes' owner device, current for the call.
+struct DevCall {
+    rt::DeviceGuard guard;
+    int dev = 0;
+    int enter(const void* p) {
+        int rc = device_of(p, &dev);
+        if (rc) return rc;
+        return guard.enter(dev);
+    }
+};
 
 }  // namespace
 
@@ -779,7 +779,7 @@ int batched_reconstruct(blbrs_batcher* b, blbrs_encoder* enc, const std::string&
 // ---------------------------------------------------------------------------------------
 extern "C" {
 
-int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out) {
+static int new_encoder(int data_shards, int parity_shards, std::vector<int> devices, blbrs_encoder** out) {
     if (!out) return fail(BLBRS_ERR_INVALID_ARG, "out is NULL");
     *out = nullptr;
     if (data_shards <= 0 || parity_shards <= 0)
@@ -792,8 +792,37 @@ int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out) {
     e->core = std::move(core);
     e->k = data_shards;
     e->m = parity_shards;
+    e->devices = std::move(devices);
     *out = e;
     return BLBRS_OK;
+}
+
+int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out) {
+    return new_encoder(data_shards, parity_shards, {}, out);
+}
+
+int blbrs_new_on(int data_shards, int parity_shards, const int* devices, int ndevices, blbrs_encoder** out) {
+    if (out) *out = nullptr;
+    if (!devices || ndevices <= 0) return fail(BLBRS_ERR_INVALID_ARG, "empty device list");
+    std::vector<int> devs(devices, devices + ndevices);
+    for (int d : devs)
+        if (d < 0) return fail(BLBRS_ERR_INVALID_ARG, "negative device id");
+    return new_encoder(data_shards, parity_shards, std::move(devs), out);
+}
+
+int blbrs_encoder_devices(blbrs_encoder* enc, int* out, int cap, int* n) {
+    if (!enc || !n || (cap > 0 && !out)) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    std::vector<int> lanes;
+    int rc = enc->lanes(&lanes);
+    if (rc) return rc;
+    *n = static_cast<int>(lanes.size());
+    for (int i = 0; i < cap && i < *n; ++i) out[i] = lanes[i];
+    return BLBRS_OK;
+}
+
+int blbrs_set_default_devices(const int* devices, int ndevices) {
+    if (ndevices < 0 || (ndevices > 0 && !devices)) return fail(BLBRS_ERR_INVALID_ARG, "bad device list");
+    return rt::set_default_devices(std::vector<int>(devices, devices + ndevices));
 }
 
 void blbrs_free(blbrs_encoder* enc) { delete enc; }
@@ -817,7 +846,7 @@ int blbrs_encode(blbrs_encoder* enc, uint8_t* const* shards, const size_t* lens)
     for (int i = 0; i < n; ++i)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     auto hp = enc->encode_plan();
-    return host_code(enc, "E", *hp, shards, S, Mode::kStore, nullptr);
+    return host_call(enc, {Step{"E", hp.get(), Mode::kStore}}, shards, S, nullptr);
 }
 
 int blbrs_verify(blbrs_encoder* enc, const uint8_t* const* shards, const size_t* lens, int* ok) {
@@ -829,7 +858,7 @@ int blbrs_verify(blbrs_encoder* enc, const uint8_t* const* shards, const size_t*
     for (int i = 0; i < n; ++i)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     auto hp = enc->encode_plan();
-    return host_code(enc, "E", *hp, const_cast<uint8_t* const*>(shards), S, Mode::kVerify, ok);
+    return host_call(enc, {Step{"E", hp.get(), Mode::kVerify}}, const_cast<uint8_t* const*>(shards), S, ok);
 }
 
 static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens, bool data_only,
@@ -850,7 +879,7 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
         if (!verify_ok) return BLBRS_OK;
         for (int i = 0; i < n; ++i)
             if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
-        return host_code(enc, "E", *ep, shards, S, Mode::kVerify, verify_ok);
+        return host_call(enc, {Step{"E", ep.get(), Mode::kVerify}}, shards, S, verify_ok);
     }
     if (npresent < enc->k) return fail(BLBRS_ERR_TOO_FEW_SHARDS, "too few shards given");
     auto hp = enc->decode_plan(present, data_only, &rc);
@@ -869,7 +898,7 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
     if (!hp->out_idx.empty()) steps.push_back(Step{plan_key(false, present, data_only), hp.get(), Mode::kStore});
     if (verify_ok) steps.push_back(Step{"E", ep.get(), Mode::kVerify});
     if (steps.empty()) return BLBRS_OK;  // data_only with only parity missing
-    rc = host_run(enc, steps, shards, S, verify_ok);
+    rc = host_call(enc, steps, shards, S, verify_ok);
     if (rc) return rc;
     for (int32_t i : hp->out_idx) lens[i] = S;
     return BLBRS_OK;
@@ -891,13 +920,11 @@ int blbrs_reconstruct_verify(blbrs_encoder* enc, uint8_t* const* shards, size_t*
 
 // ---- device-resident batched path ----
 
-static int dev_stripes_strided(const blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
-                               size_t stripe_stride, size_t batch, size_t shard_len, Stripes* st) {
+static int dev_stripes_strided(uint8_t* stripes, size_t shard_stride, size_t stripe_stride, size_t batch,
+                               size_t shard_len, Stripes* st) {
     if (!stripes) return fail(BLBRS_ERR_INVALID_ARG, "stripes is NULL");
-    const int n = enc->k + enc->m;
     if (shard_stride < shard_len || (batch > 1 && stripe_stride < shard_len))
         return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than shard length");
-    (void)n;
     st->base = stripes;
     st->shard_stride = shard_stride;
     st->stripe_stride = stripe_stride;
@@ -906,13 +933,12 @@ static int dev_stripes_strided(const blbrs_encoder* enc, uint8_t* stripes, size_
     return BLBRS_OK;
 }
 
-static int dev_run(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, const Stripes& st,
+// Runs `hp` on the current device `dev`.
+static int dev_run(blbrs_encoder* enc, int dev, const std::string& key, const HostPlan& hp, const Stripes& st,
                    size_t batch, size_t S, Mode mode, int32_t* mismatch, void* stream) {
-    int dev = 0;
-    int rc = current_dev_or_fail(&dev);
-    if (rc) return rc;
     const DevPlan* plan = nullptr;
-    if ((rc = enc->dev_plan(key, hp, dev, &plan))) return rc;
+    int rc = enc->dev_plan(key, hp, dev, &plan);
+    if (rc) return rc;
     return run_plan(*plan, st, batch, S, mode, mismatch, static_cast<hipStream_t>(stream));
 }
 
@@ -921,10 +947,22 @@ int blbrs_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, 
     if (!enc) return fail(BLBRS_ERR_INVALID_ARG, "enc is NULL");
     if (batch == 0 || shard_len == 0) return BLBRS_OK;
     Stripes st;
-    int rc = dev_stripes_strided(enc, stripes, shard_stride, stripe_stride, batch, shard_len, &st);
+    int rc = dev_stripes_strided(stripes, shard_stride, stripe_stride, batch, shard_len, &st);
     if (rc) return rc;
+    DevCall dc;
+    if ((rc = dc.enter(stripes))) return rc;
     auto hp = enc->encode_plan();
-    return dev_run(enc, "E", *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+    return dev_run(enc, dc.dev, "E", *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+}
+
+static int upload_ptrs(uint8_t* const* ptrs, size_t count, hipStream_t stream, rt::PtrLease& lease,
+                       const uint64_t** dev_out, bool* aligned) {
+    std::vector<uint64_t> v(count);
+    for (size_t i = 0; i < count; ++i) {
+        if (!ptrs[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
+        v[i] = reinterpret_cast<uint64_t>(ptrs[i]);
+    }
+    return lease.upload(v.data(), count, stream, dev_out, aligned);
 }
 
 int blbrs_encode_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
@@ -932,13 +970,16 @@ int blbrs_encode_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t
     if (!enc || !shard_ptrs) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (batch == 0 || shard_len == 0) return BLBRS_OK;
     const int n = enc->k + enc->m;
-    PtrLease lease;
-    Stripes st;
-    int rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, &st.ptrs, &st.aligned);
+    DevCall dc;
+    int rc = dc.enter(shard_ptrs[0]);
     if (rc) return rc;
+    rt::PtrLease lease;
+    Stripes st;
+    if ((rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, &st.ptrs, &st.aligned)))
+        return rc;
     st.nshards = n;
     auto hp = enc->encode_plan();
-    return dev_run(enc, "E", *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+    return dev_run(enc, dc.dev, "E", *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
 }
 
 static int dev_decode_plan(blbrs_encoder* enc, const uint8_t* present, int data_only,
@@ -967,8 +1008,10 @@ int blbrs_reconstruct_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_str
     int rc = dev_decode_plan(enc, present, data_only, &hp, &key, &nothing);
     if (rc || nothing || batch == 0 || shard_len == 0) return rc;
     Stripes st;
-    if ((rc = dev_stripes_strided(enc, stripes, shard_stride, stripe_stride, batch, shard_len, &st))) return rc;
-    return dev_run(enc, key, *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+    if ((rc = dev_stripes_strided(stripes, shard_stride, stripe_stride, batch, shard_len, &st))) return rc;
+    DevCall dc;
+    if ((rc = dc.enter(stripes))) return rc;
+    return dev_run(enc, dc.dev, key, *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
 }
 
 int blbrs_reconstruct_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
@@ -980,120 +1023,161 @@ int blbrs_reconstruct_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, s
     int rc = dev_decode_plan(enc, present, data_only, &hp, &key, &nothing);
     if (rc || nothing || batch == 0 || shard_len == 0) return rc;
     const int n = enc->k + enc->m;
-    PtrLease lease;
+    DevCall dc;
+    if ((rc = dc.enter(shard_ptrs[hp->in_idx[0]]))) return rc;
+    rt::PtrLease lease;
     Stripes st;
     if ((rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, &st.ptrs, &st.aligned)))
         return rc;
     st.nshards = n;
-    return dev_run(enc, key, *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
+    return dev_run(enc, dc.dev, key, *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
 }
 
 int blbrs_verify_dev(blbrs_encoder* enc, const uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
                      size_t batch, size_t shard_len, int32_t* mismatch_dev, void* stream) {
     if (!enc || !mismatch_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (batch == 0) return BLBRS_OK;
+    DevCall dc;
+    int rc = dc.enter(mismatch_dev);
+    if (rc) return rc;
     HIP_TRY(hipMemsetAsync(mismatch_dev, 0, batch * sizeof(int32_t), static_cast<hipStream_t>(stream)));
     if (shard_len == 0) return BLBRS_OK;
     Stripes st;
-    int rc = dev_stripes_strided(enc, const_cast<uint8_t*>(stripes), shard_stride, stripe_stride, batch,
-                                 shard_len, &st);
-    if (rc) return rc;
+    if ((rc = dev_stripes_strided(const_cast<uint8_t*>(stripes), shard_stride, stripe_stride, batch, shard_len,
+                                  &st)))
+        return rc;
     auto hp = enc->encode_plan();
-    return dev_run(enc, "E", *hp, st, batch, shard_len, Mode::kVerify, mismatch_dev, stream);
+    return dev_run(enc, dc.dev, "E", *hp, st, batch, shard_len, Mode::kVerify, mismatch_dev, stream);
 }
 
 int blbrs_verify_dev_ptrs(blbrs_encoder* enc, const uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
                           int32_t* mismatch_dev, void* stream) {
     if (!enc || !shard_ptrs || !mismatch_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (batch == 0) return BLBRS_OK;
+    DevCall dc;
+    int rc = dc.enter(mismatch_dev);
+    if (rc) return rc;
     HIP_TRY(hipMemsetAsync(mismatch_dev, 0, batch * sizeof(int32_t), static_cast<hipStream_t>(stream)));
     if (shard_len == 0) return BLBRS_OK;
     const int n = enc->k + enc->m;
-    PtrLease lease;
+    rt::PtrLease lease;
     Stripes st;
-    int rc = upload_ptrs(const_cast<uint8_t* const*>(shard_ptrs), batch * n, static_cast<hipStream_t>(stream),
-                         lease, &st.ptrs, &st.aligned);
-    if (rc) return rc;
+    if ((rc = upload_ptrs(const_cast<uint8_t* const*>(shard_ptrs), batch * n, static_cast<hipStream_t>(stream),
+                          lease, &st.ptrs, &st.aligned)))
+        return rc;
     st.nshards = n;
     auto hp = enc->encode_plan();
-    return dev_run(enc, "E", *hp, st, batch, shard_len, Mode::kVerify, mismatch_dev, stream);
+    return dev_run(enc, dc.dev, "E", *hp, st, batch, shard_len, Mode::kVerify, mismatch_dev, stream);
+}
+
+// ---- multi-device parts ----
+
+static int check_parts(const blbrs_dev_part* parts, size_t nparts, size_t shard_len) {
+    if (nparts && !parts) return fail(BLBRS_ERR_INVALID_ARG, "parts is NULL");
+    for (size_t p = 0; p < nparts; ++p) {
+        if (parts[p].batch == 0) continue;
+        Stripes st;
+        int rc = dev_stripes_strided(parts[p].stripes, parts[p].shard_stride, parts[p].stripe_stride, parts[p].batch,
+                                     shard_len, &st);
+        if (rc) return fail(rc, "part " + std::to_string(p) + ": " + rt::last_error());
+    }
+    return BLBRS_OK;
+}
+
+int blbrs_encode_parts(blbrs_encoder* enc, const blbrs_dev_part* parts, size_t nparts, size_t shard_len) {
+    if (!enc) return fail(BLBRS_ERR_INVALID_ARG, "enc is NULL");
+    int rc = check_parts(parts, nparts, shard_len);
+    if (rc || shard_len == 0) return rc;
+    for (size_t p = 0; p < nparts; ++p) {
+        const blbrs_dev_part& x = parts[p];
+        if (!x.batch) continue;
+        if ((rc = blbrs_encode_dev(enc, x.stripes, x.shard_stride, x.stripe_stride, x.batch, shard_len, x.stream)))
+            return fail(rc, "part " + std::to_string(p) + ": " + rt::last_error());
+    }
+    return BLBRS_OK;
+}
+
+int blbrs_reconstruct_parts(blbrs_encoder* enc, const blbrs_dev_part* parts, size_t nparts, size_t shard_len,
+                            const uint8_t* present, int data_only) {
+    if (!enc) return fail(BLBRS_ERR_INVALID_ARG, "enc is NULL");
+    int rc = check_parts(parts, nparts, shard_len);
+    if (rc) return rc;
+    std::shared_ptr<HostPlan> hp;
+    std::string key;
+    bool nothing = false;
+    if ((rc = dev_decode_plan(enc, present, data_only, &hp, &key, &nothing)) || nothing || shard_len == 0) return rc;
+    for (size_t p = 0; p < nparts; ++p) {
+        const blbrs_dev_part& x = parts[p];
+        if (!x.batch) continue;
+        if ((rc = blbrs_reconstruct_dev(enc, x.stripes, x.shard_stride, x.stripe_stride, x.batch, shard_len, present,
+                                        data_only, x.stream)))
+            return fail(rc, "part " + std::to_string(p) + ": " + rt::last_error());
+    }
+    return BLBRS_OK;
+}
+
+int blbrs_verify_parts(blbrs_encoder* enc, const blbrs_dev_part* parts, size_t nparts, size_t shard_len,
+                       int32_t* const* mismatch_dev) {
+    if (!enc || (nparts && !mismatch_dev)) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    int rc = check_parts(parts, nparts, shard_len);
+    if (rc) return rc;
+    for (size_t p = 0; p < nparts; ++p) {
+        const blbrs_dev_part& x = parts[p];
+        if (!x.batch) continue;
+        if ((rc = blbrs_verify_dev(enc, x.stripes, x.shard_stride, x.stripe_stride, x.batch, shard_len,
+                                   mismatch_dev[p], x.stream)))
+            return fail(rc, "part " + std::to_string(p) + ": " + rt::last_error());
+    }
+    return BLBRS_OK;
 }
 
 // ---- streaming host path ----
 
 int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
                             int nstreams) {
+    (void)nstreams;
     if (!enc || !shard_ptrs) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (batch == 0 || shard_len == 0) return BLBRS_OK;
-    const int n = enc->k + enc->m, k = enc->k;
+    const size_t n = static_cast<size_t>(enc->k + enc->m);
     for (size_t i = 0; i < batch * n; ++i)
         if (!shard_ptrs[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
-    if (nstreams < 1) nstreams = 3;
-    if (nstreams > 8) nstreams = 8;
-    int dev = 0;
-    int rc = current_dev_or_fail(&dev);
+    std::vector<int> lanes;
+    int rc = enc->lanes(&lanes);
     if (rc) return rc;
     auto hp = enc->encode_plan();
-    const DevPlan* plan = nullptr;
-    if ((rc = enc->dev_plan("E", *hp, dev, &plan))) return rc;
-
-    // Pinned stripes: one zero-copy launch over the whole batch (see host_code).
-    {
-        std::vector<uint64_t> view(batch * n, 0);
-        bool all = true;
-        for (size_t i = 0; i < batch * n && all; ++i) all = device_view(shard_ptrs[i], &view[i]);
-        if (all) {
-            hipStream_t s = nullptr;
-            HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-            {
-                PtrLease pl;
-                Stripes st;
-                st.nshards = n;
-                rc = upload_table(view.data(), view.size(), s, pl, &st.ptrs, &st.aligned);
-                if (rc == BLBRS_OK) rc = run_plan(*plan, st, batch, shard_len, Mode::kStore, nullptr, s);
-            }
-            hipError_t e = hipStreamSynchronize(s);
-            (void)hipStreamDestroy(s);
-            if (rc) return rc;
-            if (e != hipSuccess) return hip_fail(e, "zero-copy encode");
-            return BLBRS_OK;
-        }
-    }
-
-    const size_t Sp = round_up(shard_len, 256);
-    const size_t slot_bytes = static_cast<size_t>(n) * Sp;
-    std::vector<hipStream_t> streams(nstreams, nullptr);
-    uint8_t* dbuf = nullptr;
-    auto cleanup = [&]() {
-        for (auto s : streams)
-            if (s) { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); }
-        if (dbuf) (void)hipFree(dbuf);
+    const std::vector<Step> steps{Step{"E", hp.get(), Mode::kStore}};
+    // Contiguous split of the stripes over the device list (multigpu.stripe_range's rule).
+    const size_t parts = std::min(lanes.size(), batch);
+    struct Part {
+        int dev;
+        size_t start, count;
+        int rc = BLBRS_OK;
+        std::string msg;
     };
-    for (auto& s : streams) {
-        hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-        if (e != hipSuccess) { cleanup(); return hip_fail(e, "hipStreamCreate"); }
+    std::vector<Part> ps;
+    const size_t base = batch / parts, extra = batch % parts;
+    for (size_t p = 0, start = 0; p < parts; ++p) {
+        const size_t count = base + (p < extra ? 1 : 0);
+        ps.push_back(Part{lanes[p], start, count});
+        start += count;
     }
-    hipError_t e = hipMalloc(&dbuf, slot_bytes * nstreams);
-    if (e != hipSuccess) { dbuf = nullptr; cleanup(); return hip_fail(e, "hipMalloc staging"); }
-    for (size_t b = 0; b < batch && rc == BLBRS_OK; ++b) {
-        const int si = static_cast<int>(b % nstreams);
-        hipStream_t s = streams[si];
-        uint8_t* slot = dbuf + slot_bytes * si;
-        for (int i = 0; i < k && e == hipSuccess; ++i)
-            e = hipMemcpyAsync(slot + i * Sp, shard_ptrs[b * n + i], shard_len, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) { rc = hip_fail(e, "H2D"); break; }
-        Stripes st;
-        st.base = slot;
-        st.shard_stride = Sp;
-        st.stripe_stride = slot_bytes;
-        st.aligned = true;
-        rc = run_plan(*plan, st, 1, shard_len, Mode::kStore, nullptr, s);
-        for (int i = k; i < n && rc == BLBRS_OK && e == hipSuccess; ++i)
-            e = hipMemcpyAsync(shard_ptrs[b * n + i], slot + i * Sp, shard_len, hipMemcpyDeviceToHost, s);
-        if (e != hipSuccess) rc = hip_fail(e, "D2H");
-    }
-    cleanup();
-    return rc;
+    auto run_part = [&](Part& p) {
+        rt::LoadTicket ticket;
+        ticket.take(p.dev);
+        rt::DeviceGuard guard;
+        p.rc = guard.enter(p.dev);
+        if (p.rc == BLBRS_OK) p.rc = host_run(enc, steps, shard_ptrs + p.start * n, p.count, shard_len, nullptr, p.dev);
+        if (p.rc != BLBRS_OK) p.msg = rt::last_error();
+    };
+    std::vector<std::thread> th;
+    for (size_t p = 1; p < parts; ++p) th.emplace_back(run_part, std::ref(ps[p]));
+    run_part(ps[0]);
+    for (auto& t : th) t.join();
+    for (size_t p = 0; p < parts; ++p)
+        if (ps[p].rc != BLBRS_OK)
+            return fail(ps[p].rc, "device " + std::to_string(ps[p].dev) + " (stripes " + std::to_string(ps[p].start) +
+                                      ".." + std::to_string(ps[p].start + ps[p].count) + "): " + ps[p].msg);
+    return BLBRS_OK;
 }
 
 // ---- CRC-32C ----
@@ -1103,8 +1187,8 @@ int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t le
     if (batch == 0 || len == 0) return BLBRS_OK;
     if (!data || !out_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (batch > 1 && stride < len) return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than length");
-    int dev = 0;
-    int rc = current_dev_or_fail(&dev);
+    DevCall dc;
+    int rc = dc.enter(data);
     if (rc) return rc;
     if (block == 0) block = len;
     hipError_t e = crc32c_blocks(data, stride, batch, len, block, out_dev, static_cast<hipStream_t>(stream));
@@ -1118,13 +1202,13 @@ int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stri
     if (batch == 0 || shard_len == 0) return BLBRS_OK;
     if (batch > 0x7FFFFFFFull) return fail(BLBRS_ERR_INVALID_ARG, "batch too large");
     Stripes st;
-    int rc = dev_stripes_strided(enc, stripes, shard_stride, stripe_stride, batch, shard_len, &st);
+    int rc = dev_stripes_strided(stripes, shard_stride, stripe_stride, batch, shard_len, &st);
     if (rc) return rc;
-    int dev = 0;
-    if ((rc = current_dev_or_fail(&dev))) return rc;
+    DevCall dc;
+    if ((rc = dc.enter(stripes))) return rc;
     auto hp = enc->encode_plan();
     const DevPlan* plan = nullptr;
-    if ((rc = enc->dev_plan("E", *hp, dev, &plan))) return rc;
+    if ((rc = enc->dev_plan("E", *hp, dc.dev, &plan))) return rc;
     if (block == 0 || block > shard_len) block = shard_len;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     if (plan->passes.size() == 1) {
@@ -1164,26 +1248,37 @@ int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {
     if (!data || !out) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (len == 0) return BLBRS_OK;
     if (block == 0) block = len;
-    WorkerLease lease;
-    int rc = lease_worker(lease);
+    std::vector<int> lanes;
+    int rc = rt::default_devices(&lanes);
     if (rc) return rc;
-    Worker& w = *lease.w;
-    const size_t nblocks = (len + block - 1) / block;
+    static std::atomic<unsigned> rr{0};
     uint64_t view = 0;
+    int owner = -1;
+    const bool visible = rt::device_view(data, &view, &owner);
+    const int dev = owner >= 0 ? owner : lanes[rt::pick_lane(lanes, rr)];
+    rt::LoadTicket ticket;
+    ticket.take(dev);
+    rt::DeviceGuard guard;
+    if ((rc = guard.enter(dev))) return rc;
+    rt::WorkerLease w;
+    if ((rc = w.acquire(dev))) return rc;
+    rt::note_call(dev);
+    const size_t nblocks = (len + block - 1) / block;
     const uint8_t* src = nullptr;
-    if (device_view(data, &view)) {
+    if (visible) {
         src = reinterpret_cast<const uint8_t*>(view);  // pinned / device memory: in place
     } else {
-        if ((rc = w.ensure(round_up(len, 256)))) return rc;
-        HIP_TRY(hipMemcpyAsync(w.dbuf, data, len, hipMemcpyHostToDevice, w.s[0]));
-        src = w.dbuf;
+        if ((rc = w->ensure_stage(round_up(len, 256)))) return rc;
+        HIP_TRY(hipMemcpyAsync(w->stage, data, len, hipMemcpyHostToDevice, w->s[0]));
+        src = w->stage;
     }
     uint32_t* dout = nullptr;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dout), nblocks * 4, w.s[0]));
-    hipError_t e = crc32c_blocks(src, len, 1, len, block, dout, w.s[0]);
-    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, nblocks * 4, hipMemcpyDeviceToHost, w.s[0]);
-    (void)hipFreeAsync(dout, w.s[0]);
-    if (e == hipSuccess) e = hipStreamSynchronize(w.s[0]);
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dout), nblocks * 4, w->s[0]));
+    hipError_t e = crc32c_blocks(src, len, 1, len, block, dout, w->s[0]);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, nblocks * 4, hipMemcpyDeviceToHost, w->s[0]);
+    (void)hipFreeAsync(dout, w->s[0]);
+    const hipError_t f = hipStreamSynchronize(w->s[0]);
+    if (e == hipSuccess) e = f;
     if (e != hipSuccess) return hip_fail(e, "crc32c");
     return BLBRS_OK;
 }
@@ -1194,32 +1289,26 @@ int blbrs_batcher_new(int max_batch, int window_us, blbrs_batcher** out) {
     if (!out) return fail(BLBRS_ERR_INVALID_ARG, "out is NULL");
     *out = nullptr;
     if (max_batch <= 0 || window_us < 0) return fail(BLBRS_ERR_INVALID_ARG, "max_batch must be > 0, window_us >= 0");
-    int dev = 0;
-    int rc = current_dev_or_fail(&dev);
+    std::vector<int> devs;
+    int rc = rt::default_devices(&devs);
     if (rc) return rc;
-    auto* b = new blbrs_batcher();
-    b->device = dev;
-    b->max_batch = static_cast<size_t>(max_batch);
-    b->window = std::chrono::microseconds(window_us);
-    hipError_t e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-        delete b;
-        return hip_fail(e, "hipStreamCreate");
-    }
-    b->th = std::thread([b] { b->run(); });
-    *out = b;
-    return BLBRS_OK;
+    return make_batcher(max_batch, window_us, devs, out);
+}
+
+int blbrs_batcher_new_on(int max_batch, int window_us, const int* devices, int ndevices, blbrs_batcher** out) {
+    if (!out) return fail(BLBRS_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    if (max_batch <= 0 || window_us < 0) return fail(BLBRS_ERR_INVALID_ARG, "max_batch must be > 0, window_us >= 0");
+    if (!devices || ndevices <= 0) return fail(BLBRS_ERR_INVALID_ARG, "empty device list");
+    std::vector<int> devs(devices, devices + ndevices);
+    int rc = rt::check_devices(devs);
+    if (rc) return rc;
+    return make_batcher(max_batch, window_us, devs, out);
 }
 
 void blbrs_batcher_free(blbrs_batcher* b) {
     if (!b) return;
-    {
-        std::lock_guard<std::mutex> g(b->mu);
-        b->stop = true;
-    }
-    b->cv_in.notify_all();
-    b->th.join();  // drains the queue first
-    (void)hipStreamDestroy(b->stream);
+    b->shutdown();
     delete b;
 }
 
@@ -1246,11 +1335,11 @@ int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece
     }
     if (!dst || (nextents && !extents)) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (npieces > 1 && dst_stride < piece_len) return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than piece length");
-    int dev = 0;
-    int rc = current_dev_or_fail(&dev);
+    DevCall dc;
+    int rc = dc.enter(dst);
     if (rc) return rc;
     uint64_t dview = 0;
-    if (!device_view(dst, &dview)) return fail(BLBRS_ERR_INVALID_ARG, "pack destination is not device-accessible");
+    if (!rt::device_view(dst, &dview)) return fail(BLBRS_ERR_INVALID_ARG, "pack destination is not device-accessible");
     // checkTractSpec (store.go:996-1009) per piece, plus the table: piece starts, then
     // {src, offset, length, piece} per extent.
     std::vector<uint64_t> table(npieces + 1 + 4 * nextents);
@@ -1275,7 +1364,7 @@ int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece
             if (!x.src) return fail(BLBRS_ERR_INVALID_ARG, "extent " + std::to_string(i) + ": NULL source");
             if (x.src == last_src) {
                 sview = last_view;
-            } else if (!device_view(x.src, &sview)) {
+            } else if (!rt::device_view(x.src, &sview)) {
                 return fail(BLBRS_ERR_INVALID_ARG, "extent " + std::to_string(i) + ": source is not device-accessible");
             }
             last_src = x.src;
@@ -1288,12 +1377,74 @@ int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece
     }
     while (next_piece <= npieces) table[next_piece++] = nextents;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    PtrLease lease;
+    rt::PtrLease lease;
     const uint64_t* tdev = nullptr;
     bool unused = false;
-    if ((rc = upload_table(table.data(), table.size(), s, lease, &tdev, &unused))) return rc;
+    if ((rc = lease.upload(table.data(), table.size(), s, &tdev, &unused))) return rc;
     hipError_t e = pack_pieces(reinterpret_cast<uint8_t*>(dview), dst_stride, npieces, piece_len, tdev, s);
     if (e != hipSuccess) return hip_fail(e, "pack_pieces");
+    return BLBRS_OK;
+}
+
+// ---- pinned host memory ----
+
+int blbrs_buffer_get(size_t n, uint8_t** out, size_t* cap) {
+    if (!out || !cap) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    return rt::pool_get(n, out, cap);
+}
+
+int blbrs_buffer_put(uint8_t* p) { return rt::pool_put(p); }
+
+int blbrs_pool_set_idle_limit(size_t bytes) { return rt::pool_set_idle_limit(bytes); }
+
+int blbrs_get_pool_stats(blbrs_pool_stats* out) {
+    if (!out) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    return rt::pool_stats(out);
+}
+
+int blbrs_host_alloc(size_t n, void** out) {
+    if (!out || n == 0) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument or zero length");
+    *out = nullptr;
+    int nd = 0;
+    int rc = rt::device_count(&nd);
+    if (rc) return rc;
+    HIP_TRY(hipHostMalloc(out, n, hipHostMallocDefault));
+    return BLBRS_OK;
+}
+
+int blbrs_host_free(void* p) {
+    if (!p) return BLBRS_OK;
+    HIP_TRY(hipHostFree(p));
+    return BLBRS_OK;
+}
+
+int blbrs_host_register(void* p, size_t n) {
+    if (!p || n == 0) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument or zero length");
+    int nd = 0;
+    int rc = rt::device_count(&nd);
+    if (rc) return rc;
+    HIP_TRY(hipHostRegister(p, n, hipHostRegisterPortable | hipHostRegisterMapped));
+    return BLBRS_OK;
+}
+
+int blbrs_host_unregister(void* p) {
+    if (!p) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    HIP_TRY(hipHostUnregister(p));
+    return BLBRS_OK;
+}
+
+// ---- runtime limits ----
+
+int blbrs_set_worker_limit(int per_device) { return rt::set_worker_limit(per_device); }
+
+int blbrs_get_device_stats(int device, blbrs_device_stats* out) {
+    if (!out || device < 0) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
+    return rt::device_stats(device, out);
+}
+
+int blbrs_trim(void) {
+    rt::trim_workers();
+    rt::pool_trim();
     return BLBRS_OK;
 }
 
@@ -1312,9 +1463,9 @@ int blbrs_device_count(int* count) {
     return BLBRS_OK;
 }
 
-const char* blbrs_last_error(void) { return g_last_error.c_str(); }
+const char* blbrs_last_error(void) { return rt::last_error().c_str(); }
 
-const char* blbrs_version(void) { return "blbrs 0.1.0 (gfx950; klauspost/reedsolomon@925cb01d6510 semantics)"; }
+const char* blbrs_version(void) { return "blbrs 0.2.0 (gfx950; klauspost/reedsolomon@925cb01d6510 semantics)"; }
 
 const char* blbrs_strerror(int code) {
     switch (code) {

@@ -1,0 +1,592 @@
+// runtime.hip -- host runtime of libblbrs (see runtime.hpp).
+#include "runtime.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <unordered_map>
+
+namespace blbrs {
+namespace rt {
+
+// ---------------------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------------------
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return BLBRS_ERR_HIP;
+}
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+const std::string& last_error() { return g_last_error; }
+
+// ---------------------------------------------------------------------------------------
+// devices
+// ---------------------------------------------------------------------------------------
+
+namespace {
+
+std::mutex g_defaults_mu;
+std::vector<int> g_defaults;   // empty = not chosen yet
+
+constexpr int kMaxDevices = 64;
+std::atomic<int64_t> g_load[kMaxDevices];
+std::atomic<uint64_t> g_stage_bytes[kMaxDevices];
+
+void stage_add(int dev, int64_t delta) {
+    if (dev >= 0 && dev < kMaxDevices) g_stage_bytes[dev].fetch_add(static_cast<uint64_t>(delta));
+}
+
+}  // namespace
+
+int device_count(int* n) {
+    int c = 0;
+    const hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess || c <= 0) {
+        (void)hipGetLastError();
+        return fail(BLBRS_ERR_NO_DEVICE, "no HIP device visible");
+    }
+    *n = std::min(c, kMaxDevices);
+    return BLBRS_OK;
+}
+
+int check_devices(const std::vector<int>& devs) {
+    if (devs.empty()) return fail(BLBRS_ERR_INVALID_ARG, "empty device list");
+    int n = 0;
+    int rc = device_count(&n);
+    if (rc) return rc;
+    for (int d : devs)
+        if (d < 0 || d >= n)
+            return fail(BLBRS_ERR_INVALID_ARG, "device " + std::to_string(d) + " is not visible (" +
+                                                   std::to_string(n) + " devices)");
+    return BLBRS_OK;
+}
+
+int default_devices(std::vector<int>* out) {
+    std::lock_guard<std::mutex> g(g_defaults_mu);
+    if (g_defaults.empty()) {
+        int n = 0;
+        int rc = device_count(&n);
+        if (rc) return rc;
+        std::vector<int> devs;
+        if (const char* env = std::getenv("BLBRS_DEVICES"); env && *env) {
+            const char* p = env;
+            while (*p) {
+                char* end = nullptr;
+                const long d = std::strtol(p, &end, 10);
+                if (end == p) break;
+                devs.push_back(static_cast<int>(d));
+                p = *end == ',' ? end + 1 : end;
+            }
+            if ((rc = check_devices(devs))) return fail(rc, "BLBRS_DEVICES: " + last_error());
+        } else {
+            for (int d = 0; d < n; ++d) devs.push_back(d);
+        }
+        g_defaults = devs;
+    }
+    *out = g_defaults;
+    return BLBRS_OK;
+}
+
+int set_default_devices(const std::vector<int>& devs) {
+    if (!devs.empty()) {
+        int rc = check_devices(devs);
+        if (rc) return rc;
+    }
+    std::lock_guard<std::mutex> g(g_defaults_mu);
+    g_defaults = devs;  // empty: resolved again from $BLBRS_DEVICES / all visible
+    return BLBRS_OK;
+}
+
+DeviceGuard::~DeviceGuard() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+}
+
+int DeviceGuard::enter(int dev) {
+    int cur = 0;
+    BLBRS_HIP_TRY(hipGetDevice(&cur));
+    if (prev_ < 0) prev_ = cur;
+    if (cur != dev) BLBRS_HIP_TRY(hipSetDevice(dev));
+    return BLBRS_OK;
+}
+
+void load_add(int dev, int delta) {
+    if (dev >= 0 && dev < kMaxDevices) g_load[dev].fetch_add(delta, std::memory_order_relaxed);
+}
+
+int64_t load_of(int dev) {
+    return dev >= 0 && dev < kMaxDevices ? g_load[dev].load(std::memory_order_relaxed) : 0;
+}
+
+size_t pick_lane(const std::vector<int>& lanes, std::atomic<unsigned>& rr) {
+    const size_t n = lanes.size();
+    const size_t start = rr.fetch_add(1, std::memory_order_relaxed) % n;
+    size_t best = start;
+    int64_t best_load = load_of(lanes[start]);
+    for (size_t j = 1; j < n && best_load > 0; ++j) {
+        const size_t i = (start + j) % n;
+        const int64_t l = load_of(lanes[i]);
+        if (l < best_load) {
+            best = i;
+            best_load = l;
+        }
+    }
+    return best;
+}
+
+bool device_view(const void* p, uint64_t* view, int* owner) {
+    if (owner) *owner = -1;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: clear the sticky error
+        return false;
+    }
+    if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) {
+        *view = reinterpret_cast<uint64_t>(p);
+        if (owner) *owner = attr.device;
+        return true;
+    }
+    if (attr.type == hipMemoryTypeHost && attr.devicePointer && attr.hostPointer) {
+        *view = reinterpret_cast<uint64_t>(attr.devicePointer) +
+                (reinterpret_cast<uintptr_t>(p) - reinterpret_cast<uintptr_t>(attr.hostPointer));
+        return true;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------------------
+// stream workers
+// ---------------------------------------------------------------------------------------
+
+int Worker::ensure_stage(size_t bytes) {
+    if (bytes <= stage_cap) return BLBRS_OK;
+    if (stage) (void)hipFree(stage);
+    stage_add(device, -static_cast<int64_t>(stage_cap));
+    stage = nullptr;
+    stage_cap = 0;
+    BLBRS_HIP_TRY(hipMalloc(&stage, bytes));
+    stage_cap = bytes;
+    stage_add(device, static_cast<int64_t>(bytes));
+    return BLBRS_OK;
+}
+
+int Worker::upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned) {
+    if (count > tab_cap) {
+        // The previous copy out of tab_host has completed: every call that used it ended with
+        // a sync of s[0].
+        if (tab_host) (void)hipHostFree(tab_host);
+        if (tab_dev) (void)hipFree(tab_dev);
+        tab_host = nullptr;
+        tab_dev = nullptr;
+        tab_cap = 0;
+        const size_t cap = std::max<size_t>(round_up(count, 64), 256);
+        BLBRS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&tab_host), cap * 8, hipHostMallocDefault));
+        BLBRS_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&tab_dev), cap * 8));
+        tab_cap = cap;
+    }
+    bool al = true;
+    for (size_t i = 0; i < count; ++i) {
+        tab_host[i] = ptrs[i];
+        al = al && aligned16(ptrs[i]);
+    }
+    BLBRS_HIP_TRY(hipMemcpyAsync(tab_dev, tab_host, count * 8, hipMemcpyHostToDevice, s[0]));
+    *dev_out = tab_dev;
+    *aligned = al;
+    return BLBRS_OK;
+}
+
+void Worker::destroy() {
+    for (auto& x : s)
+        if (x) {
+            (void)hipStreamSynchronize(x);
+            (void)hipStreamDestroy(x);
+            x = nullptr;
+        }
+    if (flag) (void)hipFree(flag);
+    if (stage) (void)hipFree(stage);
+    if (tab_host) (void)hipHostFree(tab_host);
+    if (tab_dev) (void)hipFree(tab_dev);
+    stage_add(device, -static_cast<int64_t>(stage_cap));
+    flag = nullptr;
+    stage = nullptr;
+    tab_host = nullptr;
+    tab_dev = nullptr;
+    stage_cap = tab_cap = 0;
+}
+
+namespace {
+
+std::atomic<int> g_worker_limit{8};
+
+struct DevicePool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Worker*> idle;
+    int live = 0;  // created and not destroyed
+    uint64_t waits = 0;
+    std::atomic<uint64_t> calls{0};
+};
+
+std::mutex g_pools_mu;
+std::map<int, DevicePool*> g_pools;  // process lifetime
+
+DevicePool& pool_of(int dev) {
+    std::lock_guard<std::mutex> g(g_pools_mu);
+    auto& p = g_pools[dev];
+    if (!p) p = new DevicePool();
+    return *p;
+}
+
+// Creates a worker on the current device (== dev); on failure everything made is released.
+int make_worker(int dev, Worker** out) {
+    auto* w = new Worker();
+    w->device = dev;
+    hipError_t e = hipSuccess;
+    for (auto& x : w->s)
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&w->flag, sizeof(int32_t));
+    if (e != hipSuccess) {
+        w->destroy();
+        delete w;
+        return hip_fail(e, "stream worker setup");
+    }
+    *out = w;
+    return BLBRS_OK;
+}
+
+}  // namespace
+
+WorkerLease::~WorkerLease() {
+    if (!w_) return;
+    DevicePool& p = pool_of(w_->device);
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        p.idle.push_back(w_);
+    }
+    p.cv.notify_one();
+}
+
+int WorkerLease::acquire(int dev) {
+    DevicePool& p = pool_of(dev);
+    {
+        std::unique_lock<std::mutex> lk(p.mu);
+        bool waited = false;
+        for (;;) {
+            if (!p.idle.empty()) {
+                w_ = p.idle.back();
+                p.idle.pop_back();
+                return BLBRS_OK;
+            }
+            if (p.live < g_worker_limit.load()) {
+                ++p.live;  // reserve the slot, build outside the lock
+                break;
+            }
+            if (!waited) {
+                ++p.waits;
+                waited = true;
+            }
+            p.cv.wait(lk);
+        }
+    }
+    Worker* w = nullptr;
+    const int rc = make_worker(dev, &w);
+    if (rc) {
+        {
+            std::lock_guard<std::mutex> g(p.mu);
+            --p.live;
+        }
+        p.cv.notify_one();
+        return rc;
+    }
+    w_ = w;
+    return BLBRS_OK;
+}
+
+int set_worker_limit(int per_device) {
+    if (per_device < 1) return fail(BLBRS_ERR_INVALID_ARG, "worker limit must be >= 1");
+    g_worker_limit.store(per_device);
+    std::lock_guard<std::mutex> g(g_pools_mu);
+    for (auto& [d, p] : g_pools) p->cv.notify_all();
+    return BLBRS_OK;
+}
+
+int worker_limit() { return g_worker_limit.load(); }
+
+void note_call(int dev) { pool_of(dev).calls.fetch_add(1, std::memory_order_relaxed); }
+
+int device_stats(int dev, blbrs_device_stats* out) {
+    DevicePool& p = pool_of(dev);
+    std::lock_guard<std::mutex> g(p.mu);
+    out->workers = static_cast<uint64_t>(p.live);
+    out->idle = p.idle.size();
+    out->waits = p.waits;
+    out->staging_bytes = dev >= 0 && dev < kMaxDevices ? g_stage_bytes[dev].load() : 0;
+    out->calls = p.calls.load();
+    out->inflight = load_of(dev);
+    return BLBRS_OK;
+}
+
+void trim_workers() {
+    std::vector<std::pair<int, DevicePool*>> pools;
+    {
+        std::lock_guard<std::mutex> g(g_pools_mu);
+        for (auto& [d, p] : g_pools) pools.emplace_back(d, p);
+    }
+    for (auto& [d, p] : pools) {
+        std::vector<Worker*> idle;
+        {
+            std::lock_guard<std::mutex> g(p->mu);
+            idle.swap(p->idle);
+            p->live -= static_cast<int>(idle.size());
+        }
+        if (idle.empty()) continue;
+        DeviceGuard guard;
+        if (guard.enter(d) != BLBRS_OK) continue;
+        for (Worker* w : idle) {
+            w->destroy();
+            delete w;
+        }
+        p->cv.notify_all();
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// pointer tables on caller streams
+// ---------------------------------------------------------------------------------------
+
+struct PtrSlot {
+    std::mutex mu;
+    uint64_t* host = nullptr;
+    uint64_t* dev = nullptr;
+    size_t cap = 0;  // entries
+    hipEvent_t done = nullptr;
+};
+
+namespace {
+
+struct SlotRing {
+    static constexpr int kSlots = 16;
+    PtrSlot slots[kSlots];
+    std::atomic<unsigned> next{0};
+};
+
+std::mutex g_rings_mu;
+std::map<int, SlotRing*> g_rings;  // process lifetime
+
+SlotRing& ring_of(int dev) {
+    std::lock_guard<std::mutex> g(g_rings_mu);
+    auto& r = g_rings[dev];
+    if (!r) r = new SlotRing();
+    return *r;
+}
+
+}  // namespace
+
+PtrLease::~PtrLease() {
+    if (slot_) {
+        (void)hipEventRecord(slot_->done, stream_);
+        slot_->mu.unlock();
+    }
+}
+
+int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, const uint64_t** dev_out,
+                     bool* aligned) {
+    int dev = 0;
+    BLBRS_HIP_TRY(hipGetDevice(&dev));
+    SlotRing& r = ring_of(dev);
+    PtrSlot& s = r.slots[r.next.fetch_add(1) % SlotRing::kSlots];
+    s.mu.lock();
+    if (!s.done) {
+        const hipError_t e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            s.mu.unlock();
+            return hip_fail(e, "hipEventCreate");
+        }
+    } else {
+        const hipError_t e = hipEventSynchronize(s.done);
+        if (e != hipSuccess) {
+            s.mu.unlock();
+            return hip_fail(e, "hipEventSynchronize");
+        }
+    }
+    if (s.cap < count) {
+        if (s.host) (void)hipHostFree(s.host);
+        if (s.dev) (void)hipFree(s.dev);
+        s.host = nullptr;
+        s.dev = nullptr;
+        s.cap = 0;
+        const size_t cap = std::max<size_t>(count, 1024);
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&s.host), cap * 8, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.dev), cap * 8);
+        if (e != hipSuccess) {
+            s.mu.unlock();
+            return hip_fail(e, "ptr table alloc");
+        }
+        s.cap = cap;
+    }
+    bool al = true;
+    for (size_t i = 0; i < count; ++i) {
+        s.host[i] = ptrs[i];
+        al = al && aligned16(ptrs[i]);
+    }
+    slot_ = &s;
+    stream_ = stream;
+    BLBRS_HIP_TRY(hipMemcpyAsync(s.dev, s.host, count * 8, hipMemcpyHostToDevice, stream));
+    *dev_out = s.dev;
+    *aligned = al;
+    return BLBRS_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// pinned buffer pool -- rpc.GetBuffer / PutBuffer (pkg/rpc/pool.go:16-62)
+// ---------------------------------------------------------------------------------------
+//
+// Same capacity classes as blb's pool: 1 MiB, 4 MiB and 8 MiB (+ disk.ExtraRoom = one 64 KiB
+// ChecksumFile block, pkg/disk/checksum_file.go:27), plus a 128 KiB + ExtraRoom class for
+// the small buffers blb allocates with make() (pinning each of those separately would cost
+// more than the copy it saves).  Larger requests get an exact allocation, freed on Put.
+// Buffers are pinned and mapped for every device (hipHostMallocDefault = portable | mapped),
+// so the coding kernels read and write them in place over PCIe.  Like sync.Pool, Get never
+// blocks; idle buffers above the idle limit are freed on Put.
+
+namespace {
+
+constexpr size_t kExtraRoom = 64 << 10;
+constexpr size_t kClasses[] = {(size_t{128} << 10) + kExtraRoom, (size_t{1} << 20) + kExtraRoom,
+                               (size_t{4} << 20) + kExtraRoom, (size_t{8} << 20) + kExtraRoom};
+constexpr int kNumClasses = 4;
+
+struct HostPool {
+    std::mutex mu;
+    std::vector<uint8_t*> free_list[kNumClasses];
+    std::unordered_map<uint8_t*, size_t> live;  // every buffer handed out -> capacity
+    size_t idle_bytes = 0, live_bytes = 0;
+    size_t idle_limit = size_t{4} << 30;
+    uint64_t gets = 0, puts = 0, allocs = 0, frees = 0;
+};
+
+HostPool& host_pool() {
+    static HostPool* p = new HostPool();  // process lifetime
+    return *p;
+}
+
+int class_of(size_t cap) {
+    for (int c = 0; c < kNumClasses; ++c)
+        if (cap == kClasses[c]) return c;
+    return -1;
+}
+
+}  // namespace
+
+int pool_get(size_t n, uint8_t** out, size_t* cap) {
+    *out = nullptr;
+    if (n == 0) return fail(BLBRS_ERR_INVALID_ARG, "zero-length buffer");
+    HostPool& p = host_pool();
+    size_t want = n;
+    int c = 0;
+    while (c < kNumClasses && n > kClasses[c]) ++c;
+    if (c < kNumClasses) want = kClasses[c];
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        ++p.gets;
+        if (c < kNumClasses && !p.free_list[c].empty()) {
+            uint8_t* b = p.free_list[c].back();
+            p.free_list[c].pop_back();
+            p.idle_bytes -= want;
+            p.live[b] = want;
+            p.live_bytes += want;
+            *out = b;
+            *cap = want;
+            return BLBRS_OK;
+        }
+    }
+    int nd = 0;
+    int rc = device_count(&nd);
+    if (rc) return rc;
+    uint8_t* b = nullptr;
+    BLBRS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&b), want, hipHostMallocDefault));
+    std::lock_guard<std::mutex> g(p.mu);
+    ++p.allocs;
+    p.live[b] = want;
+    p.live_bytes += want;
+    *out = b;
+    *cap = want;
+    return BLBRS_OK;
+}
+
+int pool_put(uint8_t* b) {
+    if (!b) return BLBRS_OK;
+    HostPool& p = host_pool();
+    bool free_it = false;
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        auto it = p.live.find(b);
+        if (it == p.live.end()) return fail(BLBRS_ERR_INVALID_ARG, "buffer was not allocated by blbrs_buffer_get");
+        const size_t cap = it->second;
+        p.live.erase(it);
+        p.live_bytes -= cap;
+        ++p.puts;
+        const int c = class_of(cap);
+        if (c >= 0 && p.idle_bytes + cap <= p.idle_limit) {
+            p.free_list[c].push_back(b);
+            p.idle_bytes += cap;
+        } else {
+            free_it = true;
+            ++p.frees;
+        }
+    }
+    if (free_it) BLBRS_HIP_TRY(hipHostFree(b));
+    return BLBRS_OK;
+}
+
+int pool_set_idle_limit(size_t bytes) {
+    HostPool& p = host_pool();
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        p.idle_limit = bytes;
+    }
+    if (bytes == 0) pool_trim();
+    return BLBRS_OK;
+}
+
+int pool_stats(blbrs_pool_stats* out) {
+    HostPool& p = host_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    out->gets = p.gets;
+    out->puts = p.puts;
+    out->allocs = p.allocs;
+    out->frees = p.frees;
+    out->live_bytes = p.live_bytes;
+    out->idle_bytes = p.idle_bytes;
+    return BLBRS_OK;
+}
+
+void pool_trim() {
+    HostPool& p = host_pool();
+    std::vector<uint8_t*> drop;
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        for (auto& fl : p.free_list) {
+            drop.insert(drop.end(), fl.begin(), fl.end());
+            fl.clear();
+        }
+        p.idle_bytes = 0;
+        p.frees += drop.size();
+    }
+    for (uint8_t* b : drop) (void)hipHostFree(b);
+}
+
+}  // namespace rt
+}  // namespace blbrs

@@ -1,0 +1,156 @@
+// runtime.hpp -- the host runtime under libblbrs's C ABI: errors, device selection, the
+// bounded per-device stream-worker pool, pointer-table upload and the pinned buffer pool.
+//
+// blb calls the RS engine from many goroutines at once: one per RSEncode RPC, bounded only by
+// the tractserver's pendingSem / RejectCtlReqThreshold = 1000 (internal/tractserver/
+// config.go:91, server.go:553-582), one per curator chunk encode (internal/curator/
+// pack_tracts.go:187-196) and one per client degraded read (client/blb/reconstruct.go:65-195).
+// cgo runs each on some OS thread whose current HIP device means nothing (goroutines migrate),
+// so every call here picks its device itself and leaves the caller's current device as it
+// found it:
+//   * host-memory calls go to the least-loaded device of the encoder's device list;
+//   * device-resident calls run on the device that owns the stripes.
+// Workers (two streams, a bounded staging ring, a pointer table and a verify flag) are
+// capped per device; a call that finds none idle waits for one instead of growing HBM.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/blb_rs.h"
+
+namespace blbrs {
+namespace rt {
+
+// ---- errors (thread-local message, as blbrs_last_error() reports it) ----
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+void set_last_error(const std::string& msg);
+const std::string& last_error();
+
+#define BLBRS_HIP_TRY(expr)                                          \
+    do {                                                             \
+        hipError_t e_ = (expr);                                      \
+        if (e_ != hipSuccess) return ::blbrs::rt::hip_fail(e_, #expr); \
+    } while (0)
+
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+inline bool aligned16(uintptr_t x) { return (x & 15u) == 0; }
+
+// ---- devices ----
+
+// Number of visible HIP devices; BLBRS_ERR_NO_DEVICE when there are none.
+int device_count(int* n);
+// The process default device list: blbrs_set_default_devices(), else $BLBRS_DEVICES
+// ("0,1,..."), else every visible device.
+int default_devices(std::vector<int>* out);
+int set_default_devices(const std::vector<int>& devs);
+// Every entry in [0, device_count).
+int check_devices(const std::vector<int>& devs);
+
+// Scoped hipSetDevice: restores the calling thread's device on destruction.
+class DeviceGuard {
+ public:
+    DeviceGuard() = default;
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+    ~DeviceGuard();
+    int enter(int dev);
+
+ private:
+    int prev_ = -1;
+};
+
+// Calls in flight per device (host-memory calls and batch parts), for least-loaded choice.
+void load_add(int dev, int delta);
+int64_t load_of(int dev);
+// Index into `lanes` of the least-loaded entry; ties rotate through `rr`.
+size_t pick_lane(const std::vector<int>& lanes, std::atomic<unsigned>& rr);
+
+struct LoadTicket {
+    int dev = -1;
+    void take(int d) { dev = d; load_add(d, 1); }
+    ~LoadTicket() {
+        if (dev >= 0) load_add(dev, -1);
+    }
+};
+
+// Address under which the GPU reaches `p`: device memory as is, pinned host memory
+// (hipHostMalloc / hipHostRegister) through its device mapping.  False for pageable memory.
+// *owner = the device holding device memory, -1 for host memory.
+bool device_view(const void* p, uint64_t* view, int* owner = nullptr);
+
+// ---- stream workers ----
+
+// Staging budget per worker ring slot: k+m shards x chunk bytes fit in it.
+constexpr size_t kStageSlotBudget = size_t{16} << 20;
+
+struct Worker {
+    int device = -1;
+    hipStream_t s[2] = {nullptr, nullptr};
+    int32_t* flag = nullptr;        // verify mismatch flag (device)
+    uint8_t* stage = nullptr;       // device staging: 2 ring slots
+    size_t stage_cap = 0;
+    uint64_t* tab_host = nullptr;   // pinned pointer table
+    uint64_t* tab_dev = nullptr;
+    size_t tab_cap = 0;             // entries
+    int ensure_stage(size_t bytes);
+    // Copies `count` device addresses to the worker's device table on stream s[0].
+    int upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned);
+    void destroy();
+};
+
+// Exclusive use of one worker of `dev` for the duration of a call.  acquire() waits while
+// the device already has the maximum number of workers and none is idle.
+class WorkerLease {
+ public:
+    WorkerLease() = default;
+    WorkerLease(const WorkerLease&) = delete;
+    WorkerLease& operator=(const WorkerLease&) = delete;
+    ~WorkerLease();
+    int acquire(int dev);
+    Worker& operator*() const { return *w_; }
+    Worker* operator->() const { return w_; }
+
+ private:
+    Worker* w_ = nullptr;
+};
+
+int set_worker_limit(int per_device);
+int worker_limit();
+int device_stats(int dev, blbrs_device_stats* out);
+void note_call(int dev);
+// Frees idle workers of every device (streams, staging, tables).
+void trim_workers();
+
+// ---- pointer tables for calls on caller streams (the *_ptrs entry points) ----
+struct PtrSlot;
+class PtrLease {
+ public:
+    PtrLease() = default;
+    PtrLease(const PtrLease&) = delete;
+    PtrLease& operator=(const PtrLease&) = delete;
+    ~PtrLease();
+    // Uploads on `stream` (current device); the slot stays busy until the stream has run the
+    // kernels that read it.
+    int upload(const uint64_t* ptrs, size_t count, hipStream_t stream, const uint64_t** dev_out, bool* aligned);
+
+ private:
+    PtrSlot* slot_ = nullptr;
+    hipStream_t stream_ = nullptr;
+};
+
+// ---- pinned buffer pool (rpc.GetBuffer / PutBuffer over pinned, device-mapped memory) ----
+int pool_get(size_t n, uint8_t** out, size_t* cap);
+int pool_put(uint8_t* p);
+int pool_set_idle_limit(size_t bytes);
+int pool_stats(blbrs_pool_stats* out);
+void pool_trim();
+
+}  // namespace rt
+}  // namespace blbrs

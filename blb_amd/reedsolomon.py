@@ -113,10 +113,14 @@ def _dev_ptr(t) -> int:
 class Encoder:
     """reedsolomon.Encoder for (DataShards, ParityShards), backed by libblbrs."""
 
-    def __init__(self, data_shards: int, parity_shards: int):
+    def __init__(self, data_shards: int, parity_shards: int, devices: Optional[Sequence[int]] = None):
         self._lib = _lib.load()
         h = ctypes.c_void_p()
-        _check(self._lib.blbrs_new(int(data_shards), int(parity_shards), ctypes.byref(h)))
+        if devices is None:
+            _check(self._lib.blbrs_new(int(data_shards), int(parity_shards), ctypes.byref(h)))
+        else:
+            devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+            _check(self._lib.blbrs_new_on(int(data_shards), int(parity_shards), devs, len(devices), ctypes.byref(h)))
         self._h = h
         self.DataShards = int(data_shards)
         self.ParityShards = int(parity_shards)
@@ -135,6 +139,14 @@ class Encoder:
         self._batcher = batcher  # keep it alive while attached
 
     # ---- introspection ----
+    def Devices(self) -> list:
+        """The encoder's device list (host calls run on its least-loaded entry)."""
+        n = ctypes.c_int(0)
+        _check(self._lib.blbrs_encoder_devices(self._h, None, 0, ctypes.byref(n)))
+        out = (ctypes.c_int * max(1, n.value))()
+        _check(self._lib.blbrs_encoder_devices(self._h, out, n.value, ctypes.byref(n)))
+        return list(out[:n.value])
+
     def matrix(self) -> np.ndarray:
         out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
         _check(self._lib.blbrs_matrix(self._h, out.ctypes.data, out.size))
@@ -319,6 +331,40 @@ class Encoder:
         _check(self._lib.blbrs_verify_dev(self._h, stripes.data_ptr(), ss, bs, B, S, flags.data_ptr(), st))
         return flags == 0
 
+    # ---- multi-device parts (one [B_p, k+m, S] CUDA tensor per device share) ----
+    def _parts(self, parts):
+        arr = (_lib.DevPart * len(parts))()
+        S = None
+        for i, t in enumerate(parts):
+            B, s_, ss, bs = self._stripes(t)
+            if S is None:
+                S = s_
+            elif s_ != S:
+                raise ErrShardSize("shard sizes do not match")
+            arr[i] = _lib.DevPart(t.data_ptr(), ss, bs, B, _torch_stream(t))
+        return arr, (S or 0)
+
+    def EncodeParts(self, parts: Sequence) -> None:
+        """Encode every part in place, each on its own device and current torch stream."""
+        arr, S = self._parts(parts)
+        _check(self._lib.blbrs_encode_parts(self._h, arr, len(parts), S))
+
+    def ReconstructParts(self, parts: Sequence, present: Sequence[bool], data_only: bool = False) -> None:
+        if len(present) != self.Shards:
+            raise ErrTooFewShards("too few shards given")
+        arr, S = self._parts(parts)
+        pres = (ctypes.c_uint8 * self.Shards)(*[1 if p else 0 for p in present])
+        _check(self._lib.blbrs_reconstruct_parts(self._h, arr, len(parts), S, pres, int(data_only)))
+
+    def VerifyParts(self, parts: Sequence) -> list:
+        """[B_p] torch.bool per part: True where the stripe's parity is consistent."""
+        import torch
+        arr, S = self._parts(parts)
+        flags = [torch.empty(t.shape[0], dtype=torch.int32, device=t.device) for t in parts]
+        fp = (ctypes.c_void_p * len(parts))(*[f.data_ptr() for f in flags])
+        _check(self._lib.blbrs_verify_parts(self._h, arr, len(parts), S, fp))
+        return [f == 0 for f in flags]
+
     def EncodeHostBatch(self, stripes: Sequence[Sequence[np.ndarray]], nstreams: int = 3) -> None:
         """Streaming encode of host-resident stripes (pinned memory gives full PCIe rate)."""
         n = self.Shards
@@ -345,10 +391,15 @@ class Batcher:
     kernel launch per (shape, erasure pattern, length) group.  Attach with
     Encoder.SetBatcher; free only after detaching from every encoder."""
 
-    def __init__(self, max_batch: int = 64, window_us: int = 200):
+    def __init__(self, max_batch: int = 64, window_us: int = 200, devices: Optional[Sequence[int]] = None):
         self._lib = _lib.load()
         h = ctypes.c_void_p()
-        _check(self._lib.blbrs_batcher_new(int(max_batch), int(window_us), ctypes.byref(h)))
+        if devices is None:
+            _check(self._lib.blbrs_batcher_new(int(max_batch), int(window_us), ctypes.byref(h)))
+        else:
+            devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+            _check(self._lib.blbrs_batcher_new_on(int(max_batch), int(window_us), devs, len(devices),
+                                                  ctypes.byref(h)))
         self._h = h
 
     def stats(self) -> tuple[int, int]:
@@ -367,10 +418,54 @@ class Batcher:
         self.close()
 
 
-def New(data_shards: int, parity_shards: int) -> Encoder:
+def New(data_shards: int, parity_shards: int, devices: Optional[Sequence[int]] = None) -> Encoder:
     """reedsolomon.New(dataShards, parityShards) -> Encoder (raises ErrInvShardNum /
-    ErrMaxShardNum like the Go constructor)."""
-    return Encoder(data_shards, parity_shards)
+    ErrMaxShardNum like the Go constructor).  `devices`: the device list host calls spread
+    over (blbrs_new_on); default = the process default list (every visible device)."""
+    return Encoder(data_shards, parity_shards, devices)
+
+
+def set_default_devices(devices: Optional[Sequence[int]]) -> None:
+    devs = list(devices or [])
+    arr = (ctypes.c_int * max(1, len(devs)))(*devs)
+    _check(_lib.load().blbrs_set_default_devices(arr if devs else None, len(devs)))
+
+
+# ---- pinned buffer pool: rpc.GetBuffer / PutBuffer (pkg/rpc/pool.go:16-62) ----
+
+def GetBuffer(n: int) -> np.ndarray:
+    """A length-n uint8 array in pooled pinned memory (NOT zeroed; capacity class of blb's
+    pool).  Host-memory calls on such shards run zero-copy.  Give it back with PutBuffer and
+    do not touch it afterwards."""
+    lib = _lib.load()
+    p = ctypes.c_void_p()
+    cap = ctypes.c_size_t(0)
+    _check(lib.blbrs_buffer_get(int(n), ctypes.byref(p), ctypes.byref(cap)))
+    return np.ctypeslib.as_array((ctypes.c_uint8 * int(n)).from_address(p.value))
+
+
+def PutBuffer(buf: np.ndarray) -> None:
+    _check(_lib.load().blbrs_buffer_put(buf.__array_interface__["data"][0]))
+
+
+def pool_stats() -> dict:
+    st = _lib.PoolStats()
+    _check(_lib.load().blbrs_get_pool_stats(ctypes.byref(st)))
+    return {f: int(getattr(st, f)) for f, _ in st._fields_}
+
+
+def device_stats(device: int) -> dict:
+    st = _lib.DeviceStats()
+    _check(_lib.load().blbrs_get_device_stats(int(device), ctypes.byref(st)))
+    return {f: int(getattr(st, f)) for f, _ in st._fields_}
+
+
+def set_worker_limit(per_device: int) -> None:
+    _check(_lib.load().blbrs_set_worker_limit(int(per_device)))
+
+
+def trim() -> None:
+    _check(_lib.load().blbrs_trim())
 
 
 def set_device(device: int) -> None:

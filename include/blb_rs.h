@@ -25,8 +25,13 @@
  *   - Outputs are fully overwritten, never accumulated into (rpc.GetBuffer returns
  *     un-zeroed pooled buffers, pkg/rpc/pool.go:28-43).
  *   - No pointer is retained after a call returns (cgo rule).
- *   - All functions are thread-safe; each host-memory call picks a stream worker on the
- *     calling thread's current HIP device (blbrs_set_device()).
+ *   - All functions are thread-safe and none changes the calling thread's current HIP
+ *     device.  Host-memory calls run on the least-loaded device of the encoder's device
+ *     list (blbrs_new_on; blbrs_new takes the process default list), each on a stream worker
+ *     of that device -- at most blbrs_set_worker_limit() workers per device, further callers
+ *     wait for one.  Device-resident (*_dev) calls run on the device that owns the stripes.
+ *     cgo callers therefore need no per-thread device state (goroutines migrate between OS
+ *     threads).
  */
 #ifndef BLB_RS_H
 #define BLB_RS_H
@@ -53,12 +58,51 @@ extern "C" {
 typedef struct blbrs_encoder blbrs_encoder;
 typedef struct blbrs_batcher blbrs_batcher;
 
+/* Per-device runtime counters (blbrs_get_device_stats). */
+typedef struct {
+    uint64_t workers;        /* stream workers alive on the device (<= the worker limit) */
+    uint64_t idle;           /* of which idle */
+    uint64_t waits;          /* calls that had to wait for a free worker */
+    uint64_t staging_bytes;  /* device staging memory held by the workers */
+    uint64_t calls;          /* host-memory calls and host-batch parts run on the device */
+    int64_t inflight;        /* of which running now */
+} blbrs_device_stats;
+
+/* Pinned buffer pool counters (blbrs_get_pool_stats). */
+typedef struct {
+    uint64_t gets, puts;     /* blbrs_buffer_get / blbrs_buffer_put calls */
+    uint64_t allocs, frees;  /* pinned allocations made / released */
+    uint64_t live_bytes;     /* capacity handed out and not yet put back */
+    uint64_t idle_bytes;     /* capacity kept for reuse */
+} blbrs_pool_stats;
+
+/* One device's share of a device-resident batch (blbrs_*_parts). */
+typedef struct {
+    uint8_t* stripes;        /* device memory: shard i of stripe b at stripes + b*stripe_stride + i*shard_stride */
+    size_t shard_stride;
+    size_t stripe_stride;
+    size_t batch;            /* stripes in this part */
+    void* stream;            /* a stream of the device owning `stripes`; NULL = its null stream */
+} blbrs_dev_part;
+
 /* ---- construction (reedsolomon.New) ---- */
 
 /* reedsolomon.New(dataShards, parityShards): builds the (k+m) x k systematic matrix
  * M = V * inv(V[0:k]), V[r][c] = r^c over GF(2^8)/0x11D.  Errors: INV_SHARD_NUM when
  * k <= 0 or m <= 0, MAX_SHARD_NUM when k + m > 256. */
 int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out);
+/* reedsolomon.New on an explicit device list.  Host-memory calls of the encoder run on the
+ * least-loaded entry; blbrs_encode_host_batch splits its stripes over the entries.  Entries
+ * may repeat ([0, 0] = two lanes on GPU 0).  blbrs_new(k, m) uses the process default list:
+ * blbrs_set_default_devices(), else $BLBRS_DEVICES ("0,2,..."), else every visible device.
+ * Device ids are checked at the first call that needs a device (INVALID_ARG / NO_DEVICE). */
+int blbrs_new_on(int data_shards, int parity_shards, const int* devices, int ndevices, blbrs_encoder** out);
+/* The encoder's device list (the default list resolved): *n = its length, up to cap ids
+ * copied to out. */
+int blbrs_encoder_devices(blbrs_encoder* enc, int* out, int cap, int* n);
+/* Process default device list for blbrs_new encoders; (NULL, 0) = back to $BLBRS_DEVICES /
+ * every visible device.  Encoders created earlier keep the list they resolved. */
+int blbrs_set_default_devices(const int* devices, int ndevices);
 void blbrs_free(blbrs_encoder* enc);
 int blbrs_data_shards(const blbrs_encoder* enc);
 int blbrs_parity_shards(const blbrs_encoder* enc);
@@ -120,12 +164,53 @@ int blbrs_verify_dev(blbrs_encoder* enc, const uint8_t* stripes, size_t shard_st
 int blbrs_verify_dev_ptrs(blbrs_encoder* enc, const uint8_t* const* shard_ptrs, size_t batch,
                           size_t shard_len, int32_t* mismatch_dev, void* stream);
 
-/* ---- streaming host path (pinned host stripes -> GPU -> pinned host parity) ----
- * Encodes `batch` stripes whose k+m shards are HOST pointers (shard_ptrs stripe-major),
- * overlapping H2D copies, kernels and D2H copies over `nstreams` streams on the calling
- * thread's device.  Pinned (hipHostMalloc / hipHostRegister) buffers give full PCIe rate. */
+/* Multi-device batches: parts[p] is one device's share (the device that owns
+ * parts[p].stripes), launched asynchronously on parts[p].stream -- the caller synchronizes
+ * each part's stream.  One erasure pattern for the whole batch, as in the single-device
+ * calls.  mismatch_dev[p] is a DEVICE int32 array of parts[p].batch entries on that part's
+ * device. */
+int blbrs_encode_parts(blbrs_encoder* enc, const blbrs_dev_part* parts, size_t nparts, size_t shard_len);
+int blbrs_reconstruct_parts(blbrs_encoder* enc, const blbrs_dev_part* parts, size_t nparts, size_t shard_len,
+                            const uint8_t* present, int data_only);
+int blbrs_verify_parts(blbrs_encoder* enc, const blbrs_dev_part* parts, size_t nparts, size_t shard_len,
+                       int32_t* const* mismatch_dev);
+
+/* ---- streaming host path (host stripes -> GPU -> host parity) ----
+ * Encodes `batch` stripes whose k+m shards are HOST pointers (shard_ptrs stripe-major).  The
+ * stripes are split contiguously over the encoder's device list, one host thread per entry.
+ * Pinned (blbrs_buffer_get / blbrs_host_alloc / blbrs_host_register) stripes are coded in
+ * place over PCIe; pageable ones are staged through a stream worker (H2D, kernel and D2H of
+ * successive column chunks overlapped on its two streams).  nstreams is kept for ABI
+ * compatibility and ignored. */
 int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch,
                             size_t shard_len, int nstreams);
+
+/* ---- pinned host memory: rpc.GetBuffer / PutBuffer (pkg/rpc/pool.go:16-62) ----
+ * blb's shards come from rpc.GetBuffer: pooled, NOT zeroed, capacity classes of 1, 4 and
+ * 8 MiB + disk.ExtraRoom (64 KiB).  blbrs_buffer_get returns a buffer of the same class in
+ * pinned memory mapped for every device, so host-memory calls on it run zero-copy (the
+ * kernels read and write it over PCIe, no staging).  *cap is the class capacity (>= n).
+ * Requests above the 8 MiB class get an exact allocation that blbrs_buffer_put frees.
+ * Never blocks (like sync.Pool); idle buffers above the idle limit (default 4 GiB) are freed
+ * on put.  put of a pointer not from get is INVALID_ARG. */
+int blbrs_buffer_get(size_t n, uint8_t** out, size_t* cap);
+int blbrs_buffer_put(uint8_t* p);
+int blbrs_pool_set_idle_limit(size_t bytes);
+int blbrs_get_pool_stats(blbrs_pool_stats* out);
+/* Plain pinned allocations (hipHostMalloc, portable + mapped) and registration of existing
+ * host memory (hipHostRegister, portable + mapped) for callers with their own pools. */
+int blbrs_host_alloc(size_t n, void** out);
+int blbrs_host_free(void* p);
+int blbrs_host_register(void* p, size_t n);
+int blbrs_host_unregister(void* p);
+
+/* ---- runtime limits ---- */
+/* Maximum stream workers per device (default 8, >= 1).  Each holds two streams, a verify
+ * flag and at most 2 x 16 MiB of device staging (used for pageable shards only). */
+int blbrs_set_worker_limit(int per_device);
+int blbrs_get_device_stats(int device, blbrs_device_stats* out);
+/* Frees idle stream workers and idle pooled buffers. */
+int blbrs_trim(void);
 
 /* ---- CRC-32C (Castagnoli) of shard blocks ----
  * blb checksums every shard it writes on this path: ChecksumFile blocks of 65532 data
@@ -163,10 +248,14 @@ int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stri
  * blbrs_reconstruct / blbrs_reconstruct_data calls on that encoder go through it: same
  * arguments, results and errors, the caller still blocks until its own stripe is done --
  * the Go Encoder interface is unchanged.  (blbrs_reconstruct_verify is never batched.)
- * Pinned / device shards are used in place; pageable ones are staged by the calling thread.
- * The batcher runs on the device current at creation; free it after detaching it from
- * every encoder. */
+ * Pinned / device shards are used in place; pageable ones are staged by the calling thread
+ * through the pinned buffer pool.  Each device of the batcher has a queue drained by two
+ * lanes (own stream each), so one batch is collected while the previous one runs.  A call
+ * whose shards are device memory goes to that device's queue, any other to the shortest
+ * queue.  blbrs_batcher_new uses the process default device list.  Free a batcher after
+ * detaching it from every encoder. */
 int blbrs_batcher_new(int max_batch, int window_us, blbrs_batcher** out);
+int blbrs_batcher_new_on(int max_batch, int window_us, const int* devices, int ndevices, blbrs_batcher** out);
 void blbrs_batcher_free(blbrs_batcher* b);
 int blbrs_encoder_set_batcher(blbrs_encoder* enc, blbrs_batcher* b); /* b = NULL detaches */
 /* Counters: calls served and kernel launches issued so far. */
@@ -193,7 +282,8 @@ int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece
                    const blbrs_pack_extent* extents, size_t nextents, void* stream);
 
 /* ---- misc ---- */
-int blbrs_set_device(int device);      /* hipSetDevice for the calling thread */
+int blbrs_set_device(int device);      /* hipSetDevice for the calling thread (the library
+                                          itself never relies on it) */
 int blbrs_device_count(int* count);
 const char* blbrs_last_error(void);    /* thread-local message for the last failure */
 const char* blbrs_version(void);

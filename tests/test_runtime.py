@@ -1,0 +1,294 @@
+"""The host runtime under the C ABI (blb_amd/csrc/runtime.hip):
+
+  * device lists: encoders bound to a device list spread host calls over it and split host
+    batches across it; device-resident calls run on the stripes' device -- on the 1-GPU box
+    the list [0, 0] exercises the split (two lanes on GPU 0);
+  * the bounded stream-worker pool: 4x more concurrent callers than workers, bit-exact
+    against the oracle, device memory bounded (hipMemGetInfo before / after);
+  * the pinned buffer pool (rpc.GetBuffer / PutBuffer, pkg/rpc/pool.go:16-62): capacity
+    classes, reuse, zero-copy coding on pool buffers.
+
+Every coding result is checked against the oracle restatement (oracle/)."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import ROOT  # noqa: F401
+from blb_amd import _lib
+from blb_amd import reedsolomon as rs
+
+MIB = 1 << 20
+EXTRA = 64 << 10  # disk.ExtraRoom (pkg/disk/checksum_file.go:27)
+
+
+# ---------------------------------------------------------------- CPU: argument checks
+
+def test_new_on_argument_checks():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.blbrs_new_on(6, 3, None, 0, ctypes.byref(h)) == rs.ErrInvalidArgument.code
+    neg = (ctypes.c_int * 2)(0, -1)
+    assert lib.blbrs_new_on(6, 3, neg, 2, ctypes.byref(h)) == rs.ErrInvalidArgument.code
+    ok = (ctypes.c_int * 2)(0, 0)
+    assert lib.blbrs_new_on(0, 3, ok, 2, ctypes.byref(h)) == rs.ErrInvShardNum.code
+    assert lib.blbrs_new_on(6, 3, ok, 2, ctypes.byref(h)) == 0  # ids are checked lazily
+    lib.blbrs_free(h)
+    assert lib.blbrs_set_worker_limit(0) == rs.ErrInvalidArgument.code
+    assert lib.blbrs_set_default_devices(None, -1) == rs.ErrInvalidArgument.code
+    assert lib.blbrs_buffer_put(ctypes.c_void_p(0x1000)) == rs.ErrInvalidArgument.code
+    assert lib.blbrs_buffer_get(1, None, None) == rs.ErrInvalidArgument.code
+
+
+def test_device_calls_fail_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    enc = rs.New(6, 3, devices=[0])
+    with pytest.raises((rs.ErrNoDevice, rs.ErrHIP, rs.ErrInvalidArgument)):
+        enc.Devices()
+    with pytest.raises((rs.ErrNoDevice, rs.ErrHIP)):
+        rs.GetBuffer(4096)
+
+
+# ---------------------------------------------------------------- GPU
+
+def _oracle_parity(O, k, m, data):
+    sh = [d.copy() for d in data] + [np.zeros(data[0].size, np.uint8) for _ in range(m)]
+    O.encode(k, m, sh)
+    return sh[k:]
+
+
+@pytest.mark.gpu
+def test_device_list_lanes_concurrent_host_calls(oracle_lib):
+    """[0, 0]: two lanes on GPU 0.  Concurrent Encode / ReconstructData / Verify calls from
+    8 threads spread over the list; every result bit-exact against the oracle."""
+    k, m = 6, 3
+    enc = rs.New(k, m, devices=[0, 0])
+    assert enc.Devices() == [0, 0]
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(97531 * (t + 1))
+            for it in range(6):
+                S = [4096, 65536, 123000, 1 << 20, 98765, 4 * MIB][(t + it) % 6]
+                data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+                sh = data + [np.full(S, 0xEE, np.uint8) for _ in range(m)]
+                enc.Encode(sh)
+                ref = _oracle_parity(oracle_lib, k, m, data)
+                for j in range(m):
+                    assert np.array_equal(sh[k + j], ref[j]), f"thread {t} parity {j}"
+                assert enc.Verify(sh)
+                lost = (t + it) % k
+                orig = sh[lost].copy()
+                sh[lost] = None
+                enc.ReconstructData(sh)
+                assert np.array_equal(sh[lost], orig)
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[0]
+    st = rs.device_stats(0)
+    assert st["calls"] >= 8 * 6 * 3
+    assert st["inflight"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [False, True])
+def test_device_list_host_batch_split(oracle_lib, pinned):
+    """EncodeHostBatch splits its stripes contiguously over [0, 0] (two host threads, two
+    workers); pageable stripes go through the staging ring, pinned ones zero-copy."""
+    import torch
+    k, m, B, S = 10, 4, 7, 3 * MIB + 4100
+    enc = rs.New(k, m, devices=[0, 0])
+    rng = np.random.default_rng(11)
+    if pinned:
+        host = torch.empty((B, k + m, S), dtype=torch.uint8).pin_memory().numpy()
+    else:
+        host = np.empty((B, k + m, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
+    host[:, k:] = 0xC3
+    stripes = [[host[b, i] for i in range(k + m)] for b in range(B)]
+    enc.EncodeHostBatch(stripes)
+    for b in range(B):
+        ref = _oracle_parity(oracle_lib, k, m, [host[b, i] for i in range(k)])
+        for j in range(m):
+            assert np.array_equal(host[b, k + j], ref[j]), f"stripe {b} parity {j}"
+
+
+@pytest.mark.gpu
+def test_device_parts_split_batch(oracle_lib):
+    """EncodeParts / ReconstructParts / VerifyParts over two shares of one batch on GPU 0
+    (the multi-device form: one part per device)."""
+    import torch
+    k, m, B, S = 6, 3, 10, 70001
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    st = torch.empty((B, k + m, S), dtype=torch.uint8, device=dev)
+    st[:, :k].random_(0, 256, generator=g)
+    st[:, k:].fill_(0x5A)
+    parts = [st[:4], st[4:]]
+    enc = rs.New(k, m)
+    enc.EncodeParts(parts)
+    torch.cuda.synchronize()
+    host = st.cpu().numpy()
+    for b in range(B):
+        ref = _oracle_parity(oracle_lib, k, m, [host[b, i] for i in range(k)])
+        for j in range(m):
+            assert np.array_equal(host[b, k + j], ref[j])
+    oks = enc.VerifyParts(parts)
+    assert all(bool(o.all()) for o in oks)
+    lost = st.clone()
+    lost[:, 2].fill_(0)
+    lost[:, 7].fill_(0)
+    present = [i not in (2, 7) for i in range(k + m)]
+    enc.ReconstructParts([lost[:4], lost[4:]], present)
+    torch.cuda.synchronize()
+    assert torch.equal(lost, st)
+
+
+@pytest.mark.gpu
+def test_bounded_workers_4x_threads(oracle_lib):
+    """32 threads against a limit of 8 workers: callers wait for a worker instead of
+    creating more; results bit-exact; device memory growth bounded by the limit."""
+    import torch
+    k, m, S = 6, 3, 4 * MIB  # EncodeIncrementSize (internal/tractserver/config.go:117)
+    limit, nthreads = 8, 32
+    rs.trim()
+    rs.set_worker_limit(limit)
+    try:
+        enc = rs.New(k, m, devices=[0])
+        enc.Encode([np.ones(S, np.uint8)] * k + [np.empty(S, np.uint8) for _ in range(m)])  # plans uploaded
+        torch.cuda.synchronize()
+        free0, _ = torch.cuda.mem_get_info(0)
+        errors = []
+        barrier = threading.Barrier(nthreads)
+
+        def worker(t):
+            try:
+                rng = np.random.default_rng(1000 + t)
+                data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+                ref = _oracle_parity(oracle_lib, k, m, data)
+                barrier.wait()
+                for _ in range(3):
+                    sh = data + [np.full(S, 0xA5, np.uint8) for _ in range(m)]  # pageable: staged
+                    enc.Encode(sh)
+                    for j in range(m):
+                        assert np.array_equal(sh[k + j], ref[j]), f"thread {t} parity {j}"
+            except Exception as e:
+                errors.append(e)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors, errors[0]
+        st = rs.device_stats(0)
+        assert st["workers"] <= limit
+        assert st["waits"] > 0
+        free1, _ = torch.cuda.mem_get_info(0)
+        # per worker: 2 ring slots of (k+m) x 1 MiB staging + streams, flag, table
+        bound = limit * (2 * (k + m) * MIB + 4 * MIB) + 64 * MIB
+        assert free0 - free1 <= bound, (free0 - free1, bound)
+        assert st["staging_bytes"] <= limit * 2 * (k + m) * MIB
+    finally:
+        rs.set_worker_limit(8)
+        rs.trim()
+    assert rs.device_stats(0)["workers"] == 0
+
+
+@pytest.mark.gpu
+def test_pinned_pool_classes_and_reuse():
+    """blbrs_buffer_get keeps blb's capacity classes (1/4/8 MiB + ExtraRoom, plus a small
+    class), hands back the same buffers after PutBuffer, and frees odd sizes on put."""
+    lib = _lib.load()
+
+    def get(n):
+        p = ctypes.c_void_p()
+        cap = ctypes.c_size_t()
+        assert lib.blbrs_buffer_get(n, ctypes.byref(p), ctypes.byref(cap)) == 0
+        return p.value, cap.value
+
+    cases = [(100, (128 << 10) + EXTRA), ((128 << 10) + EXTRA, (128 << 10) + EXTRA),
+             ((128 << 10) + EXTRA + 1, MIB + EXTRA), (MIB + EXTRA, MIB + EXTRA),
+             (4 * MIB, 4 * MIB + EXTRA), (4 * MIB + EXTRA + 1, 8 * MIB + EXTRA),
+             (8 * MIB + EXTRA, 8 * MIB + EXTRA), (9 * MIB, 9 * MIB)]
+    for n, want in cases:
+        p, cap = get(n)
+        assert cap == want, (n, cap, want)
+        assert lib.blbrs_buffer_put(ctypes.c_void_p(p)) == 0
+    s0 = rs.pool_stats()
+    p1, _ = get(4 * MIB)
+    lib.blbrs_buffer_put(ctypes.c_void_p(p1))
+    p2, _ = get(4 * MIB)
+    assert p2 == p1  # reused, no new pinned allocation
+    lib.blbrs_buffer_put(ctypes.c_void_p(p2))
+    s1 = rs.pool_stats()
+    assert s1["allocs"] == s0["allocs"]
+    assert s1["live_bytes"] == 0
+    assert lib.blbrs_buffer_put(ctypes.c_void_p(p2)) == rs.ErrInvalidArgument.code  # double put
+
+
+@pytest.mark.gpu
+def test_pool_buffers_code_zero_copy(oracle_lib):
+    """rsEncodeOne with every shard from the pool (CtlRead replies and the parity buffers of
+    store.go:1096-1098): Encode, ReconstructAndVerify and ReconstructData bit-exact; the
+    calls take the zero-copy path (no staging allocated)."""
+    k, m, S = 6, 3, 4 * MIB
+    rs.trim()
+    enc = rs.New(k, m, devices=[0])
+    rng = np.random.default_rng(3)
+    sh = [rs.GetBuffer(S) for _ in range(k + m)]
+    try:
+        for i in range(k):
+            sh[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+        for j in range(m):
+            sh[k + j][:] = 0xEE  # pooled buffers are not zeroed
+        enc.Encode(sh)
+        ref = _oracle_parity(oracle_lib, k, m, [sh[i] for i in range(k)])
+        for j in range(m):
+            assert np.array_equal(sh[k + j], ref[j])
+        assert rs.device_stats(0)["staging_bytes"] == 0
+        saved = sh[1].copy()
+        work = list(sh)
+        work[1] = None
+        assert enc.ReconstructAndVerify(work, outs={1: sh[1]})
+        assert np.array_equal(sh[1], saved)
+    finally:
+        for b in sh:
+            rs.PutBuffer(b)
+
+
+@pytest.mark.gpu
+def test_batcher_on_device_list():
+    """A batcher created on an explicit device list serves a host ReconstructData call in
+    one launch (its lanes live on the listed device)."""
+    import torch
+    k, m, S = 4, 2, 4096
+    b = rs.Batcher(max_batch=8, window_us=100, devices=[0])
+    try:
+        enc = rs.New(k, m, devices=[0])
+        enc.SetBatcher(b)
+        rng = np.random.default_rng(9)
+        data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+        sh = data + [np.zeros(S, np.uint8) for _ in range(m)]
+        enc.Encode(sh)
+        ref = sh[0].copy()
+        sh[0] = None
+        enc.ReconstructData(sh)
+        assert np.array_equal(sh[0], ref)
+        r, launches = b.stats()
+        assert r == 1 and launches == 1
+        enc.SetBatcher(None)
+    finally:
+        b.close()
+    torch.cuda.synchronize()
