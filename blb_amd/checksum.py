@@ -35,22 +35,40 @@ def Checksum(data, block: int = 0):
     return out
 
 
-def ChecksumBatch(buffers, block: int = 0):
+def ChecksumBatch(buffers, block: int = 0, phase: int = 0, seeds=None):
     """[B, len] torch.uint8 CUDA tensor (rows may be strided) -> [B, nblocks] torch.int32
-    CRC bits, computed on the device on the current stream."""
+    CRC bits, computed on the device on the current stream.
+
+    phase / seeds (blbrs_crc32c_dev_at): each row is a window of a file whose byte 0 sits
+    `phase` bytes into a `block`-byte block; nblocks = ceil((phase + len) / block) and entry
+    0 continues seeds[b] (crc32.Update, pkg/disk/checksum_block.go:80).  seeds: [B] int32
+    CUDA tensor of CRC bits or None."""
     import torch
     if not (_is_torch(buffers) and buffers.is_cuda and buffers.dtype == torch.uint8 and buffers.dim() == 2):
         raise ErrInvalidArgument("expected a [B, len] torch.uint8 CUDA tensor")
     B, n = buffers.shape
     if n > 1 and buffers.stride(1) != 1:
         raise ErrInvalidArgument("row bytes must be contiguous")
+    if not block:
+        phase = 0
     blk = block or max(n, 1)
-    nb = (n + blk - 1) // blk
+    nb = (n + phase + blk - 1) // blk
     out = torch.empty((B, nb), dtype=torch.int32, device=buffers.device)
+    sp = _seeds_ptr(seeds, B, buffers.device)
     if B and n:
-        _check(_lib.load().blbrs_crc32c_dev(buffers.data_ptr(), buffers.stride(0), B, n, blk, out.data_ptr(),
-                                            _torch_stream(buffers)))
+        _check(_lib.load().blbrs_crc32c_dev_at(buffers.data_ptr(), buffers.stride(0), B, n, blk, phase, sp,
+                                               out.data_ptr(), _torch_stream(buffers)))
     return out
+
+
+def _seeds_ptr(seeds, count: int, device):
+    import torch
+    if seeds is None:
+        return None
+    if not (_is_torch(seeds) and seeds.is_cuda and seeds.dtype == torch.int32 and seeds.is_contiguous()
+            and seeds.numel() == count and seeds.device == device):
+        raise ErrInvalidArgument(f"seeds must be a contiguous int32 CUDA tensor of {count} entries")
+    return seeds.data_ptr()
 
 
 def as_uint32(t) -> np.ndarray:

@@ -140,7 +140,11 @@ class Client:
                 good += 1
                 data[i] = np.ascontiguousarray(res, dtype=np.uint8)
                 if good >= n:
-                    break  # Go cancels the context here; late replies are ignored
+                    break
+            # Go cancels the context here (reconstruct.go:154): reads not started yet are
+            # dropped, running ones finish in the pool and their replies are ignored.
+            for f in futs:
+                f.cancel()
             if good < n:
                 return TractResult(len(thisB), 0, last_err)
             try:

@@ -1182,25 +1182,47 @@ int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size
 
 // ---- CRC-32C ----
 
-int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block,
-                     uint32_t* out_dev, void* stream) {
+int blbrs_crc32c_dev_at(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block, size_t phase,
+                        const uint32_t* seeds_dev, uint32_t* out_dev, void* stream) {
     if (batch == 0 || len == 0) return BLBRS_OK;
     if (!data || !out_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (batch > 1 && stride < len) return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than length");
+    if (block == 0) {
+        block = len;
+        phase = 0;
+    }
+    if (phase >= block) return fail(BLBRS_ERR_INVALID_ARG, "phase must be smaller than the block");
     DevCall dc;
     int rc = dc.enter(data);
     if (rc) return rc;
-    if (block == 0) block = len;
-    hipError_t e = crc32c_blocks(data, stride, batch, len, block, out_dev, static_cast<hipStream_t>(stream));
+    hipError_t e = crc32c_blocks(data, stride, batch, len, block, phase, seeds_dev, out_dev,
+                                 static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "crc32c_blocks");
     return BLBRS_OK;
 }
 
+int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block,
+                     uint32_t* out_dev, void* stream) {
+    return blbrs_crc32c_dev_at(data, stride, batch, len, block, 0, nullptr, out_dev, stream);
+}
+
 int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
                          size_t batch, size_t shard_len, size_t block, uint32_t* crc_out_dev, void* stream) {
+    return blbrs_encode_crc_dev_at(enc, stripes, shard_stride, stripe_stride, batch, shard_len, block, 0, nullptr,
+                                   crc_out_dev, stream);
+}
+
+int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                            size_t batch, size_t shard_len, size_t block, size_t phase, const uint32_t* seeds_dev,
+                            uint32_t* crc_out_dev, void* stream) {
     if (!enc || !crc_out_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (batch == 0 || shard_len == 0) return BLBRS_OK;
     if (batch > 0x7FFFFFFFull) return fail(BLBRS_ERR_INVALID_ARG, "batch too large");
+    if (block == 0) {
+        block = shard_len;
+        phase = 0;
+    }
+    if (phase >= block) return fail(BLBRS_ERR_INVALID_ARG, "phase must be smaller than the block");
     Stripes st;
     int rc = dev_stripes_strided(stripes, shard_stride, stripe_stride, batch, shard_len, &st);
     if (rc) return rc;
@@ -1209,7 +1231,7 @@ int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stri
     auto hp = enc->encode_plan();
     const DevPlan* plan = nullptr;
     if ((rc = enc->dev_plan("E", *hp, dc.dev, &plan))) return rc;
-    if (block == 0 || block > shard_len) block = shard_len;
+    if (block > shard_len + phase) block = shard_len + phase;  // one block
     const hipStream_t s = static_cast<hipStream_t>(stream);
     if (plan->passes.size() == 1) {
         const DevPass& ps = plan->passes[0];
@@ -1226,6 +1248,8 @@ int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stri
         a.k = ps.k_in;
         a.rows = ps.rows;
         a.crc = crc_out_dev;
+        a.phase = phase;
+        a.seeds = seeds_dev;
         if (encode_crc_supported(a)) {
             const hipError_t e = launch_encode_crc(a, s);
             if (e != hipSuccess) return hip_fail(e, "launch encode_crc_kernel");
@@ -1235,10 +1259,11 @@ int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stri
     // Shapes without a fused instantiation (or unaligned): the coding pass, then the CRC of
     // each parity row -- same results, one more read of the parity.
     if ((rc = run_plan(*plan, st, batch, shard_len, Mode::kStore, nullptr, s))) return rc;
-    const size_t nblocks = (shard_len + block - 1) / block;
+    const size_t nblocks = (shard_len + phase + block - 1) / block;
     for (int j = 0; j < enc->m; ++j) {
         const hipError_t e = crc32c_blocks(stripes + static_cast<size_t>(enc->k + j) * shard_stride, stripe_stride,
-                                           batch, shard_len, block, crc_out_dev + j * batch * nblocks, s);
+                                           batch, shard_len, block, phase, seeds_dev ? seeds_dev + j * batch : nullptr,
+                                           crc_out_dev + j * batch * nblocks, s);
         if (e != hipSuccess) return hip_fail(e, "crc32c_blocks");
     }
     return BLBRS_OK;
@@ -1274,7 +1299,7 @@ int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {
     }
     uint32_t* dout = nullptr;
     HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dout), nblocks * 4, w->s[0]));
-    hipError_t e = crc32c_blocks(src, len, 1, len, block, dout, w->s[0]);
+    hipError_t e = crc32c_blocks(src, len, 1, len, block, 0, nullptr, dout, w->s[0]);
     if (e == hipSuccess) e = hipMemcpyAsync(out, dout, nblocks * 4, hipMemcpyDeviceToHost, w->s[0]);
     (void)hipFreeAsync(dout, w->s[0]);
     const hipError_t f = hipStreamSynchronize(w->s[0]);

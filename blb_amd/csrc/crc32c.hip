@@ -11,6 +11,15 @@
 // Kernel 2 (one lane per block): folds the block's segments with S_SEG (Horner) and applies
 // the init term.  CRC is computed byte-serially per lane, so this is LDS/VALU work, not
 // a streaming HBM kernel; it runs beside the coding kernel on the data it just wrote.
+//
+// Blocks are FILE-aligned: a buffer starts `phase` bytes into its first block (the file
+// offset of its byte 0, mod block -- rsEncodeOne writes parity windows at 4 MiB * i,
+// internal/tractserver/store.go:1028-1037,1115, and the receiver checksums 65532-byte
+// ChecksumFile blocks, pkg/disk/checksum_block.go:18-34).  All kernels work in VIRTUAL
+// coordinates v = phase + offset: the `phase` bytes before the buffer are virtual zeros,
+// which leave a raw CRC unchanged, so segment layout and folding are those of a buffer
+// starting at a block boundary; only the init term of the first block uses its real length
+// and its seed (crc32.Update(seed, ...), checksum_block.go:80 chains appends that way).
 #include "crc32c.hpp"
 #include "crc_device.hpp"
 
@@ -33,6 +42,8 @@ struct SegArgs {
     uint32_t nblocks, segs_per_block;
     const CrcConsts* c;
     uint32_t* raw;                        // [batch][nblocks][segs_per_block]
+    uint64_t phase;                       // virtual offset of byte 0 (see top)
+    const uint32_t* seeds;                // per row: crc32.Update seed of block 0 (NULL = 0)
 };
 
 constexpr int kChains = 4;                        // independent CRC chains per lane
@@ -55,16 +66,19 @@ __global__ __launch_bounds__(kThreads) void crc_segment_kernel(SegArgs a) {
     const uint32_t s = g % a.segs_per_block;
     const uint32_t blk = (g / a.segs_per_block) % a.nblocks;
     const uint64_t b = g / (static_cast<uint64_t>(a.segs_per_block) * a.nblocks);
-    const uint64_t blk_start = static_cast<uint64_t>(blk) * a.block;
-    const uint64_t blk_end = blk_start + a.block < a.len ? blk_start + a.block : a.len;
-    const uint64_t start = blk_start + static_cast<uint64_t>(s) * a.seg;
-    if (start >= blk_end) {
+    const uint64_t len_v = a.len + a.phase;
+    const uint64_t blk_start = static_cast<uint64_t>(blk) * a.block;  // virtual
+    const uint64_t blk_end = blk_start + a.block < len_v ? blk_start + a.block : len_v;
+    const uint64_t seg_start = blk_start + static_cast<uint64_t>(s) * a.seg;
+    const uint64_t seg_end = seg_start + a.seg < blk_end ? seg_start + a.seg : blk_end;
+    const uint64_t start = seg_start > a.phase ? seg_start : a.phase;  // first real byte
+    if (start >= seg_end) {
         if (tid == 0) a.raw[g] = 0u;
         return;
     }
-    const uint32_t seglen = static_cast<uint32_t>(blk_end - start < a.seg ? blk_end - start : a.seg);
+    const uint32_t seglen = static_cast<uint32_t>(seg_end - start);
     const uint32_t pad = kSegMax - seglen;        // virtual zero prefix
-    const uint8_t* src = a.data + b * a.stride + start;
+    const uint8_t* src = a.data + b * a.stride + (start - a.phase);
 
     for (uint32_t i = tid; i < 1024; i += kThreads) tab[i] = a.c->table[i >> 8][i & 255];
     for (uint32_t v4 = tid; v4 < (pad + 3) / 4; v4 += kThreads) buf[lds_dw(v4)] = 0u;
@@ -151,6 +165,7 @@ struct StreamArgs {
     uint64_t total_segs;
     const CrcConsts* c;
     uint32_t* raw;
+    uint64_t phase;  // virtual offset of byte 0 (multiple of 4)
 };
 
 struct Chunk {
@@ -196,16 +211,20 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
         const uint32_t s = static_cast<uint32_t>(g % a.segs_per_block);
         const uint32_t blk = static_cast<uint32_t>((g / a.segs_per_block) % a.nblocks);
         const uint64_t b = g / (static_cast<uint64_t>(a.segs_per_block) * a.nblocks);
+        // Virtual coordinates (phase + offset); `data_v` is never dereferenced below byte 0.
+        const uint64_t len_v = a.len + a.phase;
         const uint64_t blk_start = static_cast<uint64_t>(blk) * a.block;
-        const uint64_t blk_end = blk_start + a.block < a.len ? blk_start + a.block : a.len;
-        const uint64_t start = blk_start + static_cast<uint64_t>(s) * kWaveSeg;
-        if (start >= blk_end) {
+        const uint64_t blk_end = blk_start + a.block < len_v ? blk_start + a.block : len_v;
+        const uint64_t seg_start = blk_start + static_cast<uint64_t>(s) * kWaveSeg;
+        const uint64_t start = seg_start > a.phase ? seg_start : a.phase;  // first real byte
+        const uint64_t end = seg_start + kWaveSeg < blk_end ? seg_start + kWaveSeg : blk_end;
+        if (start >= end) {
             if (lane == 0) a.raw[g] = 0u;
             continue;
         }
-        const uint64_t end = start + kWaveSeg < blk_end ? start + kWaveSeg : blk_end;
         const uint32_t pad = static_cast<uint32_t>(kWaveSeg - (end - start));  // multiple of 4
-        const uint8_t* lane_base = a.data + b * a.stride + end - kWaveSeg + lane * kChunk;  // row 0 chunk
+        const uint8_t* row_data = a.data + b * a.stride - a.phase;  // virtual origin
+        const uint8_t* lane_base = row_data + end - kWaveSeg + lane * kChunk;  // row 0 chunk
 
         uint32_t c = 0;
         if (pad < kRowBytes) {
@@ -219,8 +238,7 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
                 // row 0's real bytes: dwords before the start have negative (wrapped) offsets,
                 // fail the range check and read as 0 -- no branches, no access before start.
                 const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t*>(a.data + b * a.stride + start), 0, static_cast<int>(kRowBytes - pad),
-                    0x00020000);
+                    const_cast<uint8_t*>(row_data + start), 0, static_cast<int>(kRowBytes - pad), 0x00020000);
                 const uint32_t o = lane * kChunk - pad;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -278,8 +296,12 @@ __global__ __launch_bounds__(kThreads) void crc_combine_kernel(SegArgs a, uint64
     const uint64_t id = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
     if (id >= total_blocks) return;
     const uint32_t blk = static_cast<uint32_t>(id % a.nblocks);
-    const uint64_t blk_start = static_cast<uint64_t>(blk) * a.block;
-    const uint64_t blk_len = (blk_start + a.block < a.len ? blk_start + a.block : a.len) - blk_start;
+    const uint64_t len_v = a.len + a.phase;
+    const uint64_t blk_start = static_cast<uint64_t>(blk) * a.block;  // virtual
+    const uint64_t blk_end = blk_start + a.block < len_v ? blk_start + a.block : len_v;
+    const uint64_t blk_len = blk_end - blk_start;
+    const uint64_t real_len = blk_end - (blk_start > a.phase ? blk_start : a.phase);
+    const uint32_t seed = blk == 0 && a.seeds ? a.seeds[id / a.nblocks] : 0u;
     const uint32_t nseg = static_cast<uint32_t>((blk_len + a.seg - 1) / a.seg);
     const uint32_t* raw = a.raw + id * a.segs_per_block;
     const cu32 segm = as_const(a.c->seg);
@@ -288,7 +310,7 @@ __global__ __launch_bounds__(kThreads) void crc_combine_kernel(SegArgs a, uint64
         const uint64_t sl = s + 1 < nseg ? a.seg : blk_len - static_cast<uint64_t>(s) * a.seg;
         acc = (sl == a.seg ? apply(segm, acc) : shift_n(a.c, acc, sl)) ^ raw[s];
     }
-    out[id] = ~(shift_n(a.c, 0xFFFFFFFFu, blk_len) ^ acc);
+    out[id] = ~(shift_n(a.c, ~seed, real_len) ^ acc);
 }
 
 // ---- host-side constants ----
@@ -404,9 +426,11 @@ hipError_t crc_consts_for(uint64_t seg, const CrcConsts** out) {
 
 hipError_t crc_combine(const CrcConsts* c, const uint32_t* raw, uint64_t len, uint64_t block, uint64_t seg,
                        uint32_t nblocks, uint32_t segs_per_block, uint64_t total_blocks, uint32_t* out,
-                       hipStream_t stream) {
+                       hipStream_t stream, uint64_t phase, const uint32_t* seeds) {
     SegArgs a{};
     a.len = len;
+    a.phase = phase;
+    a.seeds = seeds;
     a.block = block;
     a.seg = seg;
     a.nblocks = nblocks;
@@ -419,14 +443,14 @@ hipError_t crc_combine(const CrcConsts* c, const uint32_t* raw, uint64_t len, ui
 }
 
 hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, uint64_t len, uint64_t block,
-                         uint32_t* out, hipStream_t stream) {
+                         uint64_t phase, const uint32_t* seeds, uint32_t* out, hipStream_t stream) {
     if (batch == 0 || len == 0) return hipSuccess;
-    if (block == 0 || !data || !out) return hipErrorInvalidValue;
-    if (block > len) block = len;
+    if (block == 0 || !data || !out || phase >= block) return hipErrorInvalidValue;
+    if (block > len + phase) block = len + phase;  // one block; only its real length matters
     // Streaming kernel when every dwordx4 row load is 4-byte aligned (segments end at block
     // ends): blb's 65532-byte blocks and whole-shard frames of dword-multiple shards.
     const bool stream_ok = (reinterpret_cast<uintptr_t>(data) & 3u) == 0 && (stride & 3u) == 0 &&
-                           (block & 3u) == 0 && (len & 3u) == 0;
+                           (block & 3u) == 0 && (len & 3u) == 0 && (phase & 3u) == 0;
     const uint64_t seg = stream_ok ? kWaveSeg : (block < kSegMax ? block : kSegMax);
     const CrcConsts* c = nullptr;
     hipError_t e = crc_consts_for(seg, &c);
@@ -437,9 +461,11 @@ hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, u
     a.len = len;
     a.block = block;
     a.seg = seg;
-    a.nblocks = static_cast<uint32_t>((len + block - 1) / block);
+    a.nblocks = static_cast<uint32_t>((len + phase + block - 1) / block);
     a.segs_per_block = static_cast<uint32_t>((block + seg - 1) / seg);
     a.c = c;
+    a.phase = phase;
+    a.seeds = seeds;
     const uint64_t total_blocks = batch * a.nblocks;
     const uint64_t total_segs = total_blocks * a.segs_per_block;
     if (total_segs > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -454,7 +480,7 @@ hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, u
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(crc_stream_kernel),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kStreamLds));
         }
-        StreamArgs sa{data, stride, len, block, a.nblocks, a.segs_per_block, total_segs, c, a.raw};
+        StreamArgs sa{data, stride, len, block, a.nblocks, a.segs_per_block, total_segs, c, a.raw, phase};
         const uint64_t waves_needed = (total_segs + 15) / 16;  // 16 waves per workgroup
         const unsigned grid = static_cast<unsigned>(waves_needed < static_cast<uint64_t>(cus) ? waves_needed : cus);
         hipLaunchKernelGGL(crc_stream_kernel, dim3(grid), dim3(kStreamThreads), kStreamLds, stream, sa);
@@ -464,7 +490,8 @@ hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, u
     }
     e = hipGetLastError();
     if (e == hipSuccess)
-        e = crc_combine(c, a.raw, len, block, seg, a.nblocks, a.segs_per_block, total_blocks, out, stream);
+        e = crc_combine(c, a.raw, len, block, seg, a.nblocks, a.segs_per_block, total_blocks, out, stream, phase,
+                        seeds);
     hipError_t f = hipFreeAsync(a.raw, stream);
     return e != hipSuccess ? e : f;
 }

@@ -8,10 +8,12 @@
 
 namespace blbrs {
 
-// CRC of `nblocks = ceil(len / block)` consecutive blocks of each of `batch` buffers
-// (buffer b at data + b * stride).  out[b * nblocks + j].  All pointers are device pointers;
-// asynchronous on `stream`.  Returns hipSuccess or the first failure.
+// CRC of the file-aligned blocks of each of `batch` buffers (buffer b at data + b * stride,
+// `len` bytes, starting `phase` < block bytes into its first block): nblocks =
+// ceil((phase + len) / block), out[b * nblocks + j] = crc32.Update(j == 0 && seeds ?
+// seeds[b] : 0, the buffer's bytes in block j).  All pointers are device pointers (seeds may
+// be NULL); asynchronous on `stream`.  Returns hipSuccess or the first failure.
 hipError_t crc32c_blocks(const uint8_t* data, uint64_t stride, uint64_t batch, uint64_t len, uint64_t block,
-                         uint32_t* out, hipStream_t stream);
+                         uint64_t phase, const uint32_t* seeds, uint32_t* out, hipStream_t stream);
 
 }  // namespace blbrs

@@ -27,14 +27,15 @@ struct CrcConsts {
 
 // Per-segment raw CRCs -> per-block CRCs: block id of `total_blocks` (= rows * nblocks; row
 // r's block j is id r * nblocks + j) folds its raw[id * segs_per_block + s] with S_seg
-// (Horner) and applies the init term.  out[id] = crc32.Checksum(block).
+// (Horner, virtual coordinates: row bytes start `phase` into block 0) and applies the init
+// term with block 0's real length and seed.  out[id] = crc32.Update(seed, block bytes).
 hipError_t crc_consts_for(uint64_t seg, const CrcConsts** out);
 // Host: the column-major matrix S_n (feed n zero bytes), for kernels' constant tables.
 void crc_shift_matrix(uint64_t n, uint32_t col[32]);
 
 hipError_t crc_combine(const CrcConsts* c, const uint32_t* raw, uint64_t len, uint64_t block, uint64_t seg,
                        uint32_t nblocks, uint32_t segs_per_block, uint64_t total_blocks, uint32_t* out,
-                       hipStream_t stream);
+                       hipStream_t stream, uint64_t phase = 0, const uint32_t* seeds = nullptr);
 
 namespace dev {
 

@@ -352,17 +352,20 @@ std::set<std::pair<int, KernelFn>> g_attr_done;  // (device, kernel) with the LD
 
 }  // namespace
 
-bool encode_crc_supported(const EncodeCrcArgs& a) {
+static bool segment_supported(const EncodeCrcArgs& a) {
     const bool aligned = (reinterpret_cast<uintptr_t>(a.base) & 3u) == 0 && (a.shard_stride & 3u) == 0 &&
                          (a.stripe_stride & 3u) == 0 && (a.S & 3u) == 0 && (a.block & 3u) == 0;
-    return a.base && aligned && a.block > 0 && pick(a.k, a.rows) != nullptr;
+    return a.base && aligned && a.block > 0 && a.phase == 0 && pick(a.k, a.rows) != nullptr;
 }
+
+bool encode_crc_supported(const EncodeCrcArgs& a) { return encode_crc_tile_supported(a) || segment_supported(a); }
 
 hipError_t launch_encode_crc(const EncodeCrcArgs& in, hipStream_t stream) {
     if (in.B == 0 || in.S == 0) return hipSuccess;
     if (!encode_crc_supported(in) || !in.crc) return hipErrorInvalidValue;
     const bool persistent = getenv("BLBRS_EC_PERSISTENT") != nullptr;  // per call: A/B in one process
-    if (!persistent && encode_crc_tile_supported(in)) return launch_encode_crc_tile(in, stream);
+    if ((!persistent || !segment_supported(in)) && encode_crc_tile_supported(in))
+        return launch_encode_crc_tile(in, stream);
     const KernelFn fn = pick(in.k, in.rows);
     const CrcConsts* c = nullptr;
     hipError_t e = crc_consts_for(kSeg, &c);
@@ -411,7 +414,8 @@ hipError_t launch_encode_crc(const EncodeCrcArgs& in, hipStream_t stream) {
     hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEcThreads), kEcLds, stream, a);
     e = hipGetLastError();
     if (e == hipSuccess)
-        e = crc_combine(c, a.raw, a.S, a.block, kSeg, a.nblocks, a.segs_per_block, total_blocks, in.crc, stream);
+        e = crc_combine(c, a.raw, a.S, a.block, kSeg, a.nblocks, a.segs_per_block, total_blocks, in.crc, stream, 0,
+                        in.seeds);
     const hipError_t f = hipFreeAsync(a.raw, stream);
     return e != hipSuccess ? e : f;
 }

@@ -16,13 +16,16 @@ struct EncodeCrcArgs {
     uint64_t shard_stride, stripe_stride;
     uint32_t B;
     uint64_t S;               // shard length
-    uint64_t block;           // CRC block length (<= S)
+    uint64_t block;           // CRC block length
     int32_t k, rows;
-    uint32_t* crc;            // device: [rows][B][nblocks]
+    uint32_t* crc;            // device: [rows][B][nblocks], nblocks = ceil((phase + S) / block)
+    uint64_t phase = 0;       // file offset of byte 0 of each shard, mod block (< block)
+    const uint32_t* seeds = nullptr;  // device [rows][B]: crc32.Update seed of block 0, or NULL
 };
 
-// True when the fused kernel covers this shape: an instantiated (k, rows), 4-byte aligned
-// base/strides/length/block.  Otherwise the caller runs the coding pass and crc32c_blocks.
+// True when a fused kernel covers this shape: the tile-grid kernel (below), or the segment
+// kernel for an instantiated (k, rows) with 4-byte aligned base/strides/length/block and
+// phase 0.  Otherwise the caller runs the coding pass and crc32c_blocks.
 bool encode_crc_supported(const EncodeCrcArgs& a);
 
 // Launches the fused kernel plus the per-block combine on `stream`: the tile-grid kernel
@@ -30,8 +33,8 @@ bool encode_crc_supported(const EncodeCrcArgs& a);
 // BLBRS_EC_PERSISTENT=1 forces the segment kernel (A/B measurements).
 hipError_t launch_encode_crc(const EncodeCrcArgs& a, hipStream_t stream);
 
-// The tile-grid form: rows <= 4, 16-byte aligned base and strides, S a multiple of the
-// 8 KiB tile, block >= tile and a multiple of 4.
+// The tile-grid form: rows <= 4, 16-byte aligned base and strides, S a multiple of 16 (the
+// last tile may be partial), block >= the 8 KiB tile, block and phase multiples of 4.
 bool encode_crc_tile_supported(const EncodeCrcArgs& a);
 hipError_t launch_encode_crc_tile(const EncodeCrcArgs& a, hipStream_t stream);
 

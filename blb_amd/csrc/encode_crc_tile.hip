@@ -22,6 +22,13 @@
 //    the boundary is raw ^ hi.  A combine kernel then Horner-folds each block's tiles and
 //    takes the block-end part of its last tile back by S_{-n} = S_{ord - n}, ord = 2^31 - 1
 //    being the multiplicative order of x modulo the Castagnoli polynomial.
+//  * Blocks are file-aligned: shard byte 0 sits `phase` bytes into block 0 (rsEncodeOne's
+//    parity windows start at 4 MiB * i of the piece, store.go:1028-1037,1115), so the
+//    boundaries are at offsets block * n - phase; block 0's CRC continues a caller seed
+//    (crc32.Update, pkg/disk/checksum_block.go:80).  The last tile may be partial (S a
+//    multiple of 16, e.g. the 4,128,704-byte last increment of a 67,043,264-byte piece): its
+//    pieces past S are neither loaded nor stored and enter the CRC as zeros, which the
+//    combine shifts back out like any block end inside a tile.
 #include "encode_crc.hpp"
 
 #include <map>
@@ -56,7 +63,8 @@ struct TArgs {
     const int32_t* out_idx;
     uint8_t* base;
     uint64_t shard_stride, stripe_stride;
-    uint64_t S, block;
+    uint64_t S, block, phase;
+    const uint32_t* seeds;    // [j * B + b]: crc32.Update seed of block 0 (NULL = 0)
     uint32_t B, tps, xcd_remap, nblocks;
     const CrcConsts* c;
     const uint32_t* lanemat;  // [32][64] for this LC
@@ -105,7 +113,11 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     const uint32_t tile = t - b * a.tps;
     const uint64_t tile_off = static_cast<uint64_t>(tile) * kTile;
     uint8_t* stripe = a.base + static_cast<uint64_t>(b) * a.stripe_stride;
-    const uint64_t my_off = tile_off + static_cast<uint64_t>(wave) * kRow + lane_piece<LC>(lane);
+    const uint32_t in_tile = wave * kRow + lane_piece<LC>(lane);  // tile offset of piece q = 0
+    const uint64_t my_off = tile_off + in_tile;
+    // Bytes of this tile inside the shard (kTile except in a partial last tile; uniform).
+    const uint32_t lim = static_cast<uint32_t>(a.S - tile_off < kTile ? a.S - tile_off : kTile);
+    const bool full = lim == kTile;
     const ci32 in_idx = as_const(a.in_idx);
     const ci32 out_idx = as_const(a.out_idx);
 
@@ -126,7 +138,8 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
         const uint8_t* p = stripe + static_cast<uint64_t>(in_idx[c]) * a.shard_stride + my_off;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q));
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (full || in_tile + 1024u * q < lim) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q));
             x[c][4 * q] = v.x;
             x[c][4 * q + 1] = v.y;
             x[c][4 * q + 2] = v.z;
@@ -156,8 +169,10 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
         uint8_t* q = stripe + static_cast<uint64_t>(out_idx[j]) * a.shard_stride + my_off;
 #pragma unroll
         for (int u = 0; u < NQ; ++u)
-            __builtin_nontemporal_store(u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
-                                        reinterpret_cast<u32x4*>(q + 1024 * u));
+            if (full || in_tile + 1024u * u < lim)
+                __builtin_nontemporal_store(
+                    u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
+                    reinterpret_cast<u32x4*>(q + 1024 * u));
     }
 
     // CRC of this lane's LC contiguous parity bytes (tile offset LC * tid) per row.
@@ -168,7 +183,7 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     // The first block boundary after the tile start; inside the tile -> the bytes past it
     // get their own raw CRC (hi).  Only the wave whose row holds the boundary needs a masked
     // chain: in earlier waves hi = 0, in later ones hi = the full raw CRC.
-    const uint64_t nb = (tile_off / a.block + 1) * a.block;
+    const uint64_t nb = ((tile_off + a.phase) / a.block + 1) * a.block - a.phase;
     const bool split = nb < tile_off + kTile;
     const uint32_t o = split ? static_cast<uint32_t>(nb - tile_off) : kTile;
     const uint32_t o_wave = o / kRow;
@@ -265,8 +280,9 @@ __global__ __launch_bounds__(256) void tile_combine_kernel(TArgs a, uint32_t log
     if (id >= total) return;
     const uint32_t blk = static_cast<uint32_t>(id % a.nblocks);
     const uint64_t jb = id / a.nblocks;  // j * B + b
-    const uint64_t bs = static_cast<uint64_t>(blk) * a.block;
-    const uint64_t be = bs + a.block < a.S ? bs + a.block : a.S;
+    const uint64_t vs = static_cast<uint64_t>(blk) * a.block;  // file-aligned block [vs, vs + block)
+    const uint64_t bs = vs > a.phase ? vs - a.phase : 0;
+    const uint64_t be = vs + a.block - a.phase < a.S ? vs + a.block - a.phase : a.S;
     const uint32_t* raw = a.raw + jb * a.tps;
     const uint32_t* hi = a.hi + jb * a.tps;
     const cu32 st = as_const(&a.c->pow2[log2t][0]);
@@ -274,12 +290,13 @@ __global__ __launch_bounds__(256) void tile_combine_kernel(TArgs a, uint32_t log
     uint32_t acc = 0u;
     for (uint64_t i = i0; i <= i1; ++i) {
         uint32_t piece = (i << log2t) < bs ? hi[i] : raw[i];  // block starts inside tile i
-        if (((i + 1) << log2t) > be) piece ^= hi[i];           // block ends inside tile i
+        if (((i + 1) << log2t) > be && be < a.S) piece ^= hi[i];  // next block starts inside tile i
         acc = (i == i0 ? 0u : apply(st, acc)) ^ piece;
     }
     const uint64_t tail = ((i1 + 1) << log2t) - be;
     if (tail) acc = shift_n(a.c, acc, kOrd - tail);
-    out[id] = ~(shift_n(a.c, 0xFFFFFFFFu, be - bs) ^ acc);
+    const uint32_t seed = blk == 0 && a.seeds ? a.seeds[jb] : 0u;
+    out[id] = ~(shift_n(a.c, ~seed, be - bs) ^ acc);
 }
 
 using KernelFn = void (*)(TArgs);
@@ -361,12 +378,14 @@ bool order_ok() {
 bool encode_crc_tile_supported(const EncodeCrcArgs& a) {
     if (!a.base || a.k <= 0 || a.rows <= 0 || pick(a.k, a.rows) == nullptr || !order_ok()) return false;
     const uint64_t T = 256ull * static_cast<uint64_t>(lc_for(a.k, a.rows));
-    const uint64_t block = a.block < a.S ? a.block : a.S;
+    if (a.block == 0 || a.phase >= a.block) return false;
+    const bool one_block = a.block >= a.S + a.phase;
     const bool aligned = (reinterpret_cast<uintptr_t>(a.base) & 15u) == 0 && (a.shard_stride & 15u) == 0 &&
                          (a.stripe_stride & 15u) == 0;
-    // Whole tiles only, at most one block boundary per tile, boundaries on dwords.
-    return aligned && a.S >= T && a.S % T == 0 && block >= T && (block & 3u) == 0 &&
-           static_cast<uint64_t>(a.B) * (a.S / T) <= 0x7FFFFFFFull;
+    // 16-byte pieces (the last tile may be partial), at most one block boundary per tile,
+    // boundaries on dwords.
+    return aligned && a.S % 16 == 0 && (one_block || (a.block >= T && (a.block & 3u) == 0 && (a.phase & 3u) == 0)) &&
+           static_cast<uint64_t>(a.B) * ((a.S + T - 1) / T) <= 0x7FFFFFFFull;
 }
 
 hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
@@ -387,11 +406,13 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     a.shard_stride = in.shard_stride;
     a.stripe_stride = in.stripe_stride;
     a.S = in.S;
-    a.block = in.block < in.S ? in.block : in.S;
+    a.phase = in.phase;
+    a.block = in.block < in.S + in.phase ? in.block : in.S + in.phase;
+    a.seeds = in.seeds;
     a.B = in.B;
     const uint32_t log2t = lc == 64 ? 14u : 13u;
-    a.tps = static_cast<uint32_t>(in.S >> log2t);
-    a.nblocks = static_cast<uint32_t>((in.S + a.block - 1) / a.block);
+    a.tps = static_cast<uint32_t>((in.S + (uint64_t{1} << log2t) - 1) >> log2t);
+    a.nblocks = static_cast<uint32_t>((in.S + a.phase + a.block - 1) / a.block);
     a.c = c;
     a.lanemat = &tc->lanemat[lc == 64 ? 0 : 1][0][0];
     a.wavemat = &tc->wavemat[lc == 64 ? 0 : 1][0][0];

@@ -35,6 +35,16 @@ class Bytes {
         b.cap_ = cap < len ? len : cap;
         return b;
     }
+    // A buffer whose last holder releases it through `release` (pooled memory).
+    template <class Release>
+    static Bytes adopt(uint8_t* p, size_t len, size_t cap, Release release) {
+        Bytes b;
+        b.store_ = std::shared_ptr<uint8_t[]>(p, release);
+        b.base_ = p;
+        b.len_ = len;
+        b.cap_ = cap < len ? len : cap;
+        return b;
+    }
     // Copy of a byte range (like append([]byte(nil), p...)).
     static Bytes copy_of(const uint8_t* p, size_t n) {
         Bytes b = make(n);

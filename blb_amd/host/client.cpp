@@ -12,6 +12,16 @@ using core::Error;
 Client::Client(TractserverTalker* ts, ReconstructBehavior rb)
     : ts_(ts), rb_(rb), sem_free_(rb.MaxInFlight > 0 ? rb.MaxInFlight : 1) {}
 
+Client::~Client() {
+    std::unique_lock<std::mutex> g(readers_->mu);
+    readers_->cv.wait(g, [&] { return readers_->running == 0; });
+}
+
+int Client::OutstandingReads() const {
+    std::lock_guard<std::mutex> g(readers_->mu);
+    return readers_->running;
+}
+
 // reconstruct.go:166 makes a fresh encoder per call; the GPU encoder caches its device
 // plans, so one per (n, m) is kept.
 reedsolomon::Encoder* Client::encoder(int n, int m) {
@@ -34,14 +44,15 @@ bool Client::shouldReconstruct(const TractPointer& tract) const {
 }
 
 // client.go:1158-1205
-TractResult Client::readOneTractRS(const TractPointer& tract, blb::Bytes thisB, int64_t thisOffset) {
+TractResult Client::readOneTractRS(const core::ContextPtr& ctx, const TractPointer& tract, blb::Bytes thisB,
+                                   int64_t thisOffset) {
     const core::TractID rsTract = tract.Chunk.ToTractID();
     const int length = std::min(static_cast<int>(thisB.len()), static_cast<int>(tract.Length));
     const int64_t offset = static_cast<int64_t>(tract.Offset) + thisOffset;
-    auto [read, err] = ts_->ReadInto(tract.Host, rsTract, core::RSChunkVersion, thisB.slice(0, length), offset);
+    auto [read, err] = ts_->ReadInto(ctx, tract.Host, rsTract, core::RSChunkVersion, thisB.slice(0, length), offset);
     if (err != Error::NoError && err != Error::ErrEOF) {
         if (!shouldReconstruct(tract)) return {static_cast<int>(thisB.len()), 0, err};
-        return reconstructOneTract(tract, thisB, offset, length);
+        return reconstructOneTract(ctx, tract, thisB, offset, length);
     }
     for (size_t i = read; i < thisB.len(); ++i) thisB[i] = 0;  // pad with zeros
     if (static_cast<int>(tract.Length) < static_cast<int>(thisB.len())) err = Error::ErrEOF;
@@ -49,7 +60,8 @@ TractResult Client::readOneTractRS(const TractPointer& tract, blb::Bytes thisB, 
 }
 
 // reconstruct.go:65-195
-TractResult Client::reconstructOneTract(const TractPointer& tract, blb::Bytes thisB, int64_t offset, int length) {
+TractResult Client::reconstructOneTract(const core::ContextPtr& ctx, const TractPointer& tract, blb::Bytes thisB,
+                                        int64_t offset, int length) {
     {
         std::unique_lock<std::mutex> g(sem_mu_);
         sem_cv_.wait(g, [&] { return sem_free_ > 0; });
@@ -81,35 +93,47 @@ TractResult Client::reconstructOneTract(const TractPointer& tract, blb::Bytes th
     if (targetIdx < 0) return {L, 0, Error::ErrInvalidArgument};
     if (static_cast<int>(requests.size()) < n) return {L, 0, Error::ErrHostNotExist};
 
-    // Fan out reads of all other pieces; the first n good replies win.  Go cancels the
-    // context for the stragglers; here they finish and are dropped, and are joined before
-    // returning so no read outlives the call.
+    // Fan out reads of all other pieces; the first n good replies win.  As in Go
+    // (reconstruct.go:119,154) the reads get a child context that is cancelled as soon as
+    // n good pieces are in, and the call returns without waiting for the stragglers; their
+    // replies land in the shared mailbox and are dropped with it.  ~Client waits for any
+    // still running, so none outlives the client or its talker.
     struct Piece {
         int idx;
         blb::Bytes res;
         Error err;
     };
-    auto shared = std::make_shared<std::pair<std::mutex, std::vector<Piece>>>();
-    auto cv = std::make_shared<std::condition_variable>();
-    struct Joiner {
-        std::vector<std::thread> t;
-        ~Joiner() {
-            for (auto& x : t) x.join();
-        }
-    } readers;
+    struct Mailbox {
+        std::mutex mu;
+        std::condition_variable cv;
+        std::vector<Piece> pieces;
+    };
+    auto box = std::make_shared<Mailbox>();
+    auto nctx = core::Background();  // context.WithCancel(ctx)
+    if (ctx && ctx->Done()) nctx->Cancel();
+    struct CancelOnReturn {
+        core::ContextPtr c;
+        ~CancelOnReturn() { c->Cancel(); }
+    } cancel{nctx};
     for (int i : requests) {
         const core::TractID id = tract.BaseChunk.Add(i).ToTractID();
         const std::string host = tract.OtherHosts[i];
-        readers.t.emplace_back([this, i, id, host, offset, length, shared, cv]() {
-            auto [res, err] = ts_->Read(host, id, core::RSChunkVersion, length, offset);
+        {
+            std::lock_guard<std::mutex> g(readers_->mu);
+            ++readers_->running;
+        }
+        std::thread([ts = ts_, readers = readers_, i, id, host, offset, length, box, nctx]() {
+            auto [res, err] = ts->Read(nctx, host, id, core::RSChunkVersion, length, offset);
             if ((err == Error::NoError || err == Error::ErrEOF) && static_cast<int>(res.len()) != length)
                 err = Error::ErrShortRead;
             {
-                std::lock_guard<std::mutex> g(shared->first);
-                shared->second.push_back(Piece{i, res, err});
+                std::lock_guard<std::mutex> g(box->mu);
+                box->pieces.push_back(Piece{i, res, err});
             }
-            cv->notify_all();
-        });
+            box->cv.notify_all();
+            std::lock_guard<std::mutex> g(readers->mu);
+            if (--readers->running == 0) readers->cv.notify_all();
+        }).detach();
     }
     reedsolomon::Shards data(n + m);
     Error lastErr = Error::NoError;
@@ -118,9 +142,9 @@ TractResult Client::reconstructOneTract(const TractPointer& tract, blb::Bytes th
     while (good < n && inFlight > 0) {
         Piece p;
         {
-            std::unique_lock<std::mutex> g(shared->first);
-            cv->wait(g, [&] { return shared->second.size() > consumed; });
-            p = shared->second[consumed++];
+            std::unique_lock<std::mutex> g(box->mu);
+            box->cv.wait(g, [&] { return box->pieces.size() > consumed; });
+            p = box->pieces[consumed++];
         }
         --inFlight;
         if (p.err != Error::NoError && p.err != Error::ErrEOF) {
@@ -130,6 +154,7 @@ TractResult Client::reconstructOneTract(const TractPointer& tract, blb::Bytes th
         ++good;
         data[p.idx] = p.res;
     }
+    nctx->Cancel();  // reconstruct.go:154
     if (good < n) return {L, 0, lastErr};
 
     reedsolomon::Encoder* enc = encoder(n, m);

@@ -37,13 +37,16 @@ struct TractResult {
     core::Error err = core::Error::NoError;
 };
 
+// The two TractserverTalker calls of the RS read path (client/blb/tractserver_talker.go).
+// ctx is cancelled once a reconstruct has the n pieces it needs (reconstruct.go:154); a
+// talker may return early then.
 class TractserverTalker {
  public:
     virtual ~TractserverTalker() = default;
-    virtual std::pair<blb::Bytes, core::Error> Read(const std::string& addr, core::TractID id, int version,
-                                                    int length, int64_t off) = 0;
-    virtual std::pair<int, core::Error> ReadInto(const std::string& addr, core::TractID id, int version,
-                                                 blb::Bytes b, int64_t off) = 0;
+    virtual std::pair<blb::Bytes, core::Error> Read(const core::ContextPtr& ctx, const std::string& addr,
+                                                    core::TractID id, int version, int length, int64_t off) = 0;
+    virtual std::pair<int, core::Error> ReadInto(const core::ContextPtr& ctx, const std::string& addr,
+                                                 core::TractID id, int version, blb::Bytes b, int64_t off) = 0;
 };
 
 // reconstruct.go:24-28
@@ -55,12 +58,25 @@ struct ReconstructBehavior {
 class Client {
  public:
     Client(TractserverTalker* ts, ReconstructBehavior rb);
+    // Waits for straggler piece reads still running (they were cancelled when their
+    // reconstruct returned), so none outlives the client or its talker.
+    ~Client();
     bool shouldReconstruct(const TractPointer& tract) const;
-    TractResult readOneTractRS(const TractPointer& tract, blb::Bytes thisB, int64_t thisOffset);
-    TractResult reconstructOneTract(const TractPointer& tract, blb::Bytes thisB, int64_t offset, int length);
+    TractResult readOneTractRS(const core::ContextPtr& ctx, const TractPointer& tract, blb::Bytes thisB,
+                               int64_t thisOffset);
+    TractResult reconstructOneTract(const core::ContextPtr& ctx, const TractPointer& tract, blb::Bytes thisB,
+                                    int64_t offset, int length);
     int Reconstructs() const { return reconstructs_; }
+    // Piece reads started by reconstructs and not finished yet.
+    int OutstandingReads() const;
 
  private:
+    struct Readers {
+        std::mutex mu;
+        std::condition_variable cv;
+        int running = 0;
+    };
+    std::shared_ptr<Readers> readers_ = std::make_shared<Readers>();
     reedsolomon::Encoder* encoder(int n, int m);
     TractserverTalker* ts_;
     ReconstructBehavior rb_;

@@ -1,6 +1,8 @@
 // core.hpp -- the slice of blb's internal/core the RS path touches (C++ restatement).
 #pragma once
+#include <atomic>
 #include <cstdint>
+#include <memory>
 #include <string>
 
 namespace core {
@@ -59,6 +61,16 @@ struct RSChunkID {
                        static_cast<uint16_t>(ID & 0xffff)};
     }
 };
+
+// context.Context, as far as the RS path uses it: cancellation of the client's straggler
+// piece reads (client/blb/reconstruct.go:119,154).
+struct Context {
+    std::atomic<bool> cancelled{false};
+    bool Done() const { return cancelled.load(); }
+    void Cancel() { cancelled.store(true); }
+};
+using ContextPtr = std::shared_ptr<Context>;
+inline ContextPtr Background() { return std::make_shared<Context>(); }
 
 struct TSAddr {
     uint64_t ID = 0;

@@ -1,6 +1,8 @@
 // tractserver.cpp -- Store::RSEncode over the GPU engine (see tractserver.hpp).
 #include "tractserver.hpp"
 
+#include "rpc.hpp"
+
 #include <algorithm>
 #include <future>
 #include <thread>
@@ -47,8 +49,12 @@ Error Store::RSEncode(core::RSChunkID baseid, int length, const std::vector<core
         return Error::NoError;
     }
 
-    // Pipelined: gather(i+1) and scatter(i-1) run on their own threads while window i is
-    // coded on the GPU.  Each stage keeps the reference's order of calls per window.
+    // Pipelined: window i+1's reads run while window i's writes are in flight, and window
+    // i's coding overlaps window i-1's writes.  Window i+1's reads start only once window i
+    // has been coded AND window i-1's writes have succeeded, so a failing read or coding
+    // step issues exactly the reference's calls (store.go:1029-1036 stops at the first
+    // failing window).  The one difference: when a CtlWrite of window i-1 fails, window i's
+    // reads have already been issued (side-effect free); no write of window i is ever sent.
     if (windows.empty()) return Error::NoError;
     auto start_gather = [&](size_t i) {
         auto w = std::make_shared<Window>();
@@ -65,13 +71,13 @@ Error Store::RSEncode(core::RSChunkID baseid, int length, const std::vector<core
     for (size_t i = 0; i < windows.size(); ++i) {
         std::shared_ptr<Window> w = next.get();
         if (w->err != Error::NoError) { result = w->err; break; }
-        if (i + 1 < windows.size()) next = start_gather(i + 1);
         Error err = code(*enc, encode, imap, N, *w);
         if (err != Error::NoError) { result = err; break; }
         if (pending_write.valid()) {
             err = pending_write.get();
             if (err != Error::NoError) { result = err; break; }
         }
+        if (i + 1 < windows.size()) next = start_gather(i + 1);
         pending_write = std::async(std::launch::async, [this, w, baseid, &dests, &imap, N]() {
             return scatter(baseid, dests, imap, N, *w);
         });
@@ -112,11 +118,12 @@ Error Store::gather(core::RSChunkID baseid, const std::vector<core::TSAddr>& src
 }
 
 // store.go:1092-1108: Encode into fresh (pooled, un-zeroed) parity buffers, or
-// reconstructAndVerify; any coding error is ErrUnknown.
+// reconstructAndVerify; any coding error is ErrUnknown.  The parity buffers come from
+// rpc::GetBuffer (pinned pool), so the GPU writes them in place.
 Error Store::code(reedsolomon::Encoder& enc, bool encode, const std::vector<int>& imap, int N, Window& w) {
     if (encode) {
         for (size_t j = N; j < imap.size(); ++j) {
-            blb::Bytes b = blb::Bytes::make(w.length);
+            blb::Bytes b = rpc::GetBuffer(w.length);
             std::fill(b.data(), b.data() + b.len(), uint8_t{0xA5});  // rpc.GetBuffer: stale contents
             w.data[imap[j]] = b;
         }

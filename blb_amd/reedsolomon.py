@@ -294,21 +294,36 @@ class Encoder:
         st = _torch_stream(stripes) if stream is None else stream
         _check(self._lib.blbrs_encode_dev(self._h, stripes.data_ptr(), ss, bs, B, S, st))
 
-    def EncodeBatchCRC(self, stripes, block: int = 0, stream: Optional[int] = None):
+    def EncodeBatchCRC(self, stripes, block: int = 0, stream: Optional[int] = None, phase: int = 0,
+                       seeds=None):
         """EncodeBatch fused with the CRC-32C of the parity it writes (one HBM pass).
 
         Returns a [m, B, nblocks] torch.int32 CUDA tensor (the uint32 CRCs' bit patterns):
         entry [j, b, i] = crc32.Checksum(block i of parity shard k+j of stripe b).
         block = 0: one block per shard (the bulk RPC frame CRC, pkg/rpc/bulk_codec.go:47);
-        65532 = ChecksumFile blocks (pkg/disk/checksum_block.go:18-34)."""
+        65532 = ChecksumFile blocks (pkg/disk/checksum_block.go:18-34).
+
+        phase / seeds (blbrs_encode_crc_dev_at): the shards are a window of the parity piece
+        whose byte 0 sits `phase` bytes into a block (rsEncodeOne's window at offset 4 MiB*i:
+        phase = 4 MiB*i mod 65532); nblocks = ceil((phase + S) / block) and entry [j, b, 0]
+        continues seeds[j, b] (crc32.Update).  seeds: [m, B] int32 CUDA tensor or None."""
         import torch
         B, S, ss, bs = self._stripes(stripes)
-        blk = S if block <= 0 or block > S else block
-        nblocks = (S + blk - 1) // blk if S else 0
+        if block <= 0:
+            blk, phase = S, 0
+        else:
+            blk = block
+        nblocks = (S + phase + blk - 1) // blk if S else 0
         out = torch.empty((self.ParityShards, B, nblocks), dtype=torch.int32, device=stripes.device)
         st = _torch_stream(stripes) if stream is None else stream
-        _check(self._lib.blbrs_encode_crc_dev(self._h, stripes.data_ptr(), ss, bs, B, S, blk,
-                                              out.data_ptr(), st))
+        sp = None
+        if seeds is not None:
+            if not (_is_torch(seeds) and seeds.dtype == torch.int32 and seeds.is_contiguous()
+                    and tuple(seeds.shape) == (self.ParityShards, B) and seeds.device == stripes.device):
+                raise ErrInvalidArgument("seeds must be a contiguous [m, B] int32 tensor on the stripes' device")
+            sp = seeds.data_ptr()
+        _check(self._lib.blbrs_encode_crc_dev_at(self._h, stripes.data_ptr(), ss, bs, B, S, blk, phase, sp,
+                                                 out.data_ptr(), st))
         return out
 
     def ReconstructBatch(self, stripes, present: Sequence[bool], data_only: bool = False,

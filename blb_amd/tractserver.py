@@ -16,9 +16,11 @@ chunk is assembled on the GPU (blb_amd.pack.PackPieces) and kept HBM-resident in
 store's local chunk table, readable through `read` (the Store.Read slice the reference's
 PackTracts test uses).
 
-`pipeline=True` overlaps the reads of window i+1 and the writes of
-window i-1 with the GPU coding of window i.  Bytes written are identical; only the
-schedule differs from the reference's strictly sequential loop.
+`pipeline=True` overlaps the reads of window i+1 with the writes of
+window i, and the GPU coding of window i with the writes of window i-1.  Bytes written are
+identical.  A failing read or coding step issues exactly the reference's calls; when a
+CtlWrite of window i-1 fails, window i's reads have already been issued (no write of
+window i is sent).
 """
 from __future__ import annotations
 
@@ -238,7 +240,7 @@ class Store:
         return self._scatter(baseid, offset, dests, imap, N, data)
 
     def _rs_encode_pipelined(self, baseid, windows, srcs, dests, index_map, enc) -> Error:
-        """Three-stage software pipeline over windows: gather(i+1) || code(i) || scatter(i-1)."""
+        """Software pipeline over windows: gather(i+1) || scatter(i), code(i) || scatter(i-1)."""
         N, M = len(srcs), len(dests)
         imap, encode = self._index_map(N, M, index_map)
         if imap is None:
@@ -251,9 +253,6 @@ class Store:
                 data, err = nxt.result()
                 if err != Error.NoError:
                     return err
-                if i + 1 < len(windows):
-                    o2, l2 = windows[i + 1]
-                    nxt = stage.submit(self._gather, baseid, o2, l2, srcs, imap, N, M)
                 err = self._code(enc, data, encode, imap, N, ln)
                 if err != Error.NoError:
                     return err
@@ -261,6 +260,11 @@ class Store:
                     err = pending_write.result()
                     if err != Error.NoError:
                         return err
+                # Window i+1's reads start only after window i is coded and window i-1's
+                # writes succeeded (store.go:1029-1036 stops at the first failing window).
+                if i + 1 < len(windows):
+                    o2, l2 = windows[i + 1]
+                    nxt = stage.submit(self._gather, baseid, o2, l2, srcs, imap, N, M)
                 pending_write = stage.submit(self._scatter, baseid, off, dests, imap, N, data)
             return pending_write.result() if pending_write is not None else Error.NoError
         finally:

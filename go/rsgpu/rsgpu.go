@@ -8,8 +8,19 @@
 //	internal/tractserver/store.go:1022   enc, e := reedsolomon.New(N, M)  ->  rsgpu.New(N, M)
 //	client/blb/reconstruct.go:166        enc, e := reedsolomon.New(n, m)  ->  rsgpu.New(n, m)
 //
+// and, so that the shards those calls see are pinned and coded in place over PCIe, blb's RPC
+// buffer pool:
+//
+//	pkg/rpc/pool.go:30   GetBuffer(n)            ->  rsgpu.GetBuffer(n)
+//	pkg/rpc/pool.go:51   PutBuffer(b, exclusive) ->  rsgpu.PutBuffer(b, exclusive)
+//
+// Every encoder spreads its calls over all visible GPUs (the library picks the least-loaded
+// device per call; no goroutine or OS thread carries device state).  NewOn binds an encoder
+// to an explicit device list.
+//
 // The returned value satisfies reedsolomon.Encoder (store.go:1042,1132 take that type).
-// Split / Join / Update are not on blb's path; they are delegated to klauspost's CPU encoder.
+// Split / Join / Update are not on blb's path; they are delegated to klauspost's CPU encoder,
+// built on first use only.
 //
 // Source only in this repository: this image has no Go toolchain (SURVEY.md §0.4).  Build
 // where Go >= 1.21 (runtime.Pinner) and the library exist:
@@ -29,6 +40,7 @@ import (
 	"errors"
 	"io"
 	"runtime"
+	"sync"
 	"sync/atomic"
 	"unsafe"
 
@@ -38,20 +50,94 @@ import (
 // batcher, when set by EnableBatching, is attached to every encoder New returns.
 var batcher atomic.Pointer[C.blbrs_batcher]
 
+// errSingular carries klauspost's message for a singular decode matrix ("matrix is
+// singular", matrix.go).  It is declared here because the pinned module version keeps its
+// own value unexported; callers only log it (store.go:1105, reconstruct.go:177).
+var errSingular = errors.New("matrix is singular")
+
+// call runs one C entry point with the goroutine locked to its OS thread, so that the
+// thread-local message blbrs_last_error() reports belongs to this call.
+func call(f func() C.int) error {
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
+	return mapErr(f())
+}
+
+// Map the C ABI's codes (blb_rs.h) back onto klauspost's exported error values, so
+// callers comparing against reedsolomon.ErrTooFewShards etc. keep working.  Must run on
+// the OS thread that made the failing call (see call).
+func mapErr(rc C.int) error {
+	switch rc {
+	case C.BLBRS_OK:
+		return nil
+	case C.BLBRS_ERR_INV_SHARD_NUM:
+		return reedsolomon.ErrInvShardNum
+	case C.BLBRS_ERR_MAX_SHARD_NUM:
+		return reedsolomon.ErrMaxShardNum
+	case C.BLBRS_ERR_TOO_FEW_SHARDS:
+		return reedsolomon.ErrTooFewShards
+	case C.BLBRS_ERR_SHARD_NO_DATA:
+		return reedsolomon.ErrShardNoData
+	case C.BLBRS_ERR_SHARD_SIZE:
+		return reedsolomon.ErrShardSize
+	case C.BLBRS_ERR_SINGULAR:
+		return errSingular
+	default:
+		return errors.New("rsgpu: " + C.GoString(C.blbrs_last_error()))
+	}
+}
+
 // EnableBatching makes every encoder created afterwards route its Reconstruct /
-// ReconstructData calls through one process-wide batcher (blb_rs.h: blbrs_batcher_new):
-// concurrent degraded reads (client/blb/reconstruct.go with ReconstructBehavior.MaxInFlight
-// > 1) then share kernel launches.  Call once at client start-up, before reads begin.
+// ReconstructData calls through one process-wide batcher over all visible GPUs (blb_rs.h:
+// blbrs_batcher_new): concurrent degraded reads (client/blb/reconstruct.go with
+// ReconstructBehavior.MaxInFlight > 1) then share kernel launches.  Call once at client
+// start-up, before reads begin.
 func EnableBatching(maxBatch, windowMicros int) error {
 	var b *C.blbrs_batcher
-	if rc := C.blbrs_batcher_new(C.int(maxBatch), C.int(windowMicros), &b); rc != C.BLBRS_OK {
-		return mapErr(rc)
+	if err := call(func() C.int { return C.blbrs_batcher_new(C.int(maxBatch), C.int(windowMicros), &b) }); err != nil {
+		return err
 	}
 	if !batcher.CompareAndSwap(nil, b) {
 		C.blbrs_batcher_free(b)
 		return errors.New("rsgpu: batching already enabled")
 	}
 	return nil
+}
+
+// SetWorkerLimit caps the stream workers per GPU (blbrs_set_worker_limit; default 8).
+// Calls beyond the cap wait for a worker, the way the tractserver's pendingSem bounds RPCs.
+func SetWorkerLimit(perDevice int) error {
+	return call(func() C.int { return C.blbrs_set_worker_limit(C.int(perDevice)) })
+}
+
+// ---- pinned buffer pool: pkg/rpc/pool.go's GetBuffer / PutBuffer ----
+
+// GetBuffer returns a []byte with length n and capacity >= n (blb's pool classes: 1, 4 and
+// 8 MiB + disk.ExtraRoom) in pinned host memory mapped for every GPU.  The buffer may not be
+// zeroed!  The memory is C memory: cgo calls may pass it freely, and shards built on it are
+// coded in place (zero-copy) by Encode / Reconstruct*.  It falls back to make() when no GPU
+// is usable, so callers never see an error.
+func GetBuffer(n int) []byte {
+	if n <= 0 {
+		return make([]byte, n)
+	}
+	var p *C.uint8_t
+	var capacity C.size_t
+	if C.blbrs_buffer_get(C.size_t(n), &p, &capacity) != C.BLBRS_OK {
+		return make([]byte, n)
+	}
+	return unsafe.Slice((*byte)(unsafe.Pointer(p)), int(capacity))[:n]
+}
+
+// PutBuffer returns a buffer to the pool.  As in pkg/rpc/pool.go it is fine to call on any
+// buffer that is not used again; non-exclusive or Go-allocated buffers are left alone.
+func PutBuffer(b []byte, exclusive bool) {
+	if !exclusive || cap(b) == 0 {
+		return
+	}
+	// blbrs_buffer_put ignores (INVALID_ARG) pointers it did not hand out, such as the
+	// make() fallback above.
+	C.blbrs_buffer_put((*C.uint8_t)(unsafe.Pointer(&b[:1][0])))
 }
 
 // ChecksumBlocks returns crc32.Checksum(block, castagnoliTable) for every `block`-byte block
@@ -70,63 +156,71 @@ func ChecksumBlocks(b []byte, block int) ([]uint32, error) {
 	pin.Pin(&b[0])
 	pin.Pin(&out[0])
 	defer pin.Unpin()
-	rc := C.blbrs_crc32c((*C.uint8_t)(unsafe.Pointer(&b[0])), C.size_t(len(b)), C.size_t(block),
-		(*C.uint32_t)(unsafe.Pointer(&out[0])))
-	return out, mapErr(rc)
-}
-
-// Map the C ABI's codes (blb_rs.h) back onto klauspost's exported error values, so
-// callers comparing against reedsolomon.ErrTooFewShards etc. keep working.
-func mapErr(rc C.int) error {
-	switch rc {
-	case C.BLBRS_OK:
-		return nil
-	case C.BLBRS_ERR_INV_SHARD_NUM:
-		return reedsolomon.ErrInvShardNum
-	case C.BLBRS_ERR_MAX_SHARD_NUM:
-		return reedsolomon.ErrMaxShardNum
-	case C.BLBRS_ERR_TOO_FEW_SHARDS:
-		return reedsolomon.ErrTooFewShards
-	case C.BLBRS_ERR_SHARD_NO_DATA:
-		return reedsolomon.ErrShardNoData
-	case C.BLBRS_ERR_SHARD_SIZE:
-		return reedsolomon.ErrShardSize
-	default:
-		return errors.New("rsgpu: " + C.GoString(C.blbrs_last_error()))
-	}
+	err := call(func() C.int {
+		return C.blbrs_crc32c((*C.uint8_t)(unsafe.Pointer(&b[0])), C.size_t(len(b)), C.size_t(block),
+			(*C.uint32_t)(unsafe.Pointer(&out[0])))
+	})
+	return out, err
 }
 
 type encoder struct {
-	h   *C.blbrs_encoder
-	k   int
-	m   int
-	cpu reedsolomon.Encoder // Split / Join / Update only
+	h       *C.blbrs_encoder
+	k       int
+	m       int
+	cpuOnce sync.Once
+	cpu     reedsolomon.Encoder // Split / Join / Update only, built on first use
+	cpuErr  error
 }
 
-// New is reedsolomon.New(dataShards, parityShards) backed by the GPU engine.
+// New is reedsolomon.New(dataShards, parityShards) backed by the GPU engine, spreading its
+// calls over every visible GPU ($BLBRS_DEVICES narrows the list).
 func New(dataShards, parityShards int) (reedsolomon.Encoder, error) {
 	var h *C.blbrs_encoder
-	if rc := C.blbrs_new(C.int(dataShards), C.int(parityShards), &h); rc != C.BLBRS_OK {
-		return nil, mapErr(rc)
-	}
-	cpu, err := reedsolomon.New(dataShards, parityShards)
-	if err != nil {
-		C.blbrs_free(h)
+	if err := call(func() C.int { return C.blbrs_new(C.int(dataShards), C.int(parityShards), &h) }); err != nil {
 		return nil, err
 	}
+	return wrap(h, dataShards, parityShards), nil
+}
+
+// NewOn is New bound to an explicit device list (entries may repeat).
+func NewOn(dataShards, parityShards int, devices []int) (reedsolomon.Encoder, error) {
+	if len(devices) == 0 {
+		return New(dataShards, parityShards)
+	}
+	devs := make([]C.int, len(devices))
+	for i, d := range devices {
+		devs[i] = C.int(d)
+	}
+	var h *C.blbrs_encoder
+	err := call(func() C.int {
+		return C.blbrs_new_on(C.int(dataShards), C.int(parityShards), &devs[0], C.int(len(devs)), &h)
+	})
+	if err != nil {
+		return nil, err
+	}
+	return wrap(h, dataShards, parityShards), nil
+}
+
+func wrap(h *C.blbrs_encoder, k, m int) *encoder {
 	if b := batcher.Load(); b != nil {
 		C.blbrs_encoder_set_batcher(h, b)
 	}
-	e := &encoder{h: h, k: dataShards, m: parityShards, cpu: cpu}
+	e := &encoder{h: h, k: k, m: m}
 	runtime.SetFinalizer(e, func(e *encoder) { C.blbrs_free(e.h) })
-	return e, nil
+	return e
+}
+
+func (e *encoder) cpuEncoder() (reedsolomon.Encoder, error) {
+	e.cpuOnce.Do(func() { e.cpu, e.cpuErr = reedsolomon.New(e.k, e.m) })
+	return e.cpu, e.cpuErr
 }
 
 // marshal builds C arrays of shard pointers and lengths.  cgo forbids storing Go pointers
-// in C memory unless they are pinned, so every non-empty shard is pinned for the call;
-// the C side does not retain any pointer after returning.  A missing shard that has
-// capacity (klauspost reslices shards[i][0:size] when cap >= size; client/blb/
-// reconstruct.go:172 relies on it) passes its backing array as the output buffer.
+// in C memory unless they are pinned, so every non-empty shard is pinned for the call
+// (Pin does nothing for pool buffers, which are C memory); the C side does not retain any
+// pointer after returning.  A missing shard that has capacity (klauspost reslices
+// shards[i][0:size] when cap >= size; client/blb/reconstruct.go:172 relies on it) passes its
+// backing array as the output buffer.
 type marshalled struct {
 	ptrs   *unsafe.Pointer
 	lens   *C.size_t
@@ -174,7 +268,7 @@ func (e *encoder) Encode(shards [][]byte) error {
 	}
 	mm := marshal(shards, shardSize(shards))
 	defer mm.free()
-	return mapErr(C.blbrs_encode(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens))
+	return call(func() C.int { return C.blbrs_encode(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens) })
 }
 
 func (e *encoder) Verify(shards [][]byte) (bool, error) {
@@ -184,8 +278,11 @@ func (e *encoder) Verify(shards [][]byte) (bool, error) {
 	mm := marshal(shards, shardSize(shards))
 	defer mm.free()
 	var ok C.int
-	if rc := C.blbrs_verify(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens, &ok); rc != C.BLBRS_OK {
-		return false, mapErr(rc)
+	err := call(func() C.int {
+		return C.blbrs_verify(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens, &ok)
+	})
+	if err != nil {
+		return false, err
 	}
 	return ok != 0, nil
 }
@@ -213,14 +310,14 @@ func (e *encoder) reconstruct(shards [][]byte, dataOnly bool) error {
 	}
 	mm := marshal(shards, size)
 	defer mm.free()
-	var rc C.int
-	if dataOnly {
-		rc = C.blbrs_reconstruct_data(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens)
-	} else {
-		rc = C.blbrs_reconstruct(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens)
-	}
-	if rc != C.BLBRS_OK {
-		return mapErr(rc)
+	err := call(func() C.int {
+		if dataOnly {
+			return C.blbrs_reconstruct_data(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens)
+		}
+		return C.blbrs_reconstruct(e.h, (**C.uint8_t)(unsafe.Pointer(mm.ptrs)), mm.lens)
+	})
+	if err != nil {
+		return err
 	}
 	lens := unsafe.Slice(mm.lens, len(shards))
 	for i := range shards {
@@ -235,9 +332,25 @@ func (e *encoder) Reconstruct(shards [][]byte) error     { return e.reconstruct(
 func (e *encoder) ReconstructData(shards [][]byte) error { return e.reconstruct(shards, true) }
 
 func (e *encoder) Update(shards [][]byte, newDatashards [][]byte) error {
-	return e.cpu.Update(shards, newDatashards)
+	cpu, err := e.cpuEncoder()
+	if err != nil {
+		return err
+	}
+	return cpu.Update(shards, newDatashards)
 }
-func (e *encoder) Split(data []byte) ([][]byte, error) { return e.cpu.Split(data) }
+
+func (e *encoder) Split(data []byte) ([][]byte, error) {
+	cpu, err := e.cpuEncoder()
+	if err != nil {
+		return nil, err
+	}
+	return cpu.Split(data)
+}
+
 func (e *encoder) Join(dst io.Writer, shards [][]byte, outSize int) error {
-	return e.cpu.Join(dst, shards, outSize)
+	cpu, err := e.cpuEncoder()
+	if err != nil {
+		return err
+	}
+	return cpu.Join(dst, shards, outSize)
 }

@@ -218,7 +218,8 @@ int blbrs_trim(void);
  * bulk_codec.go:47, block = whole buffer).  For each of `batch` buffers (buffer b at
  * data + b * stride, `len` bytes), out[b * nblocks + j] = crc32.Checksum(block j,
  * crc32.MakeTable(crc32.Castagnoli)) with nblocks = ceil(len / block); the last block of a
- * buffer may be short.  block == 0 means one block per buffer. */
+ * buffer may be short.  block == 0 means one block per buffer.  Blocks start at byte 0 of
+ * each buffer: for a buffer that starts inside a file block use blbrs_crc32c_dev_at. */
 int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block,
                      uint32_t* out_dev, void* stream);
 /* Host-memory form: one buffer; out (host) has ceil(len / block) entries. */
@@ -234,10 +235,30 @@ int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out);
  *     crc_out_dev[(j * batch + b) * nblocks + i] = CRC-32C of block i of parity shard k+j
  *                                                  of stripe b.
  * Shapes without a fused kernel fall back to the coding pass plus blbrs_crc32c_dev's kernel
- * (same results). */
+ * (same results).  Blocks start at byte 0 of each shard; parity windows at other file
+ * offsets use blbrs_encode_crc_dev_at. */
 int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
                          size_t stripe_stride, size_t batch, size_t shard_len, size_t block,
                          uint32_t* crc_out_dev, void* stream);
+
+/* File-aligned continuation forms of the two calls above, for buffers that are a window of a
+ * file (rsEncodeOne writes parity window i at offset 4 MiB * i of the piece, store.go:1028-
+ * 1037,1115, and 4 MiB mod 65532 = 256): byte 0 of every buffer sits `phase` bytes into its
+ * first block (phase = file offset mod block, < block), so
+ *     nblocks = ceil((phase + len) / block)
+ * and block i covers the buffer bytes [max(0, i*block - phase), min(len, (i+1)*block - phase)).
+ * Entry i = crc32.Update(i == 0 ? seed : 0, castagnoliTable, those bytes) -- the ChecksumFile
+ * append rule b.cksum = crc32.Update(b.cksum, ...) (pkg/disk/checksum_block.go:76-81): pass
+ * the CRC the file's partial last block already has as the seed (for window w+1, the last
+ * entry window w produced), and block 0's entry is that block's new checksum.  seeds_dev is a
+ * DEVICE array (NULL = all 0 = plain crc32.Checksum): one per buffer for blbrs_crc32c_dev_at,
+ * [j * batch + b] per parity shard for blbrs_encode_crc_dev_at.  block == 0 = one block per
+ * buffer (phase ignored).  phase >= block is INVALID_ARG. */
+int blbrs_crc32c_dev_at(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block,
+                        size_t phase, const uint32_t* seeds_dev, uint32_t* out_dev, void* stream);
+int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
+                            size_t stripe_stride, size_t batch, size_t shard_len, size_t block,
+                            size_t phase, const uint32_t* seeds_dev, uint32_t* crc_out_dev, void* stream);
 
 /* ---- batched client reconstructs ----
  * client/blb/reconstruct.go:65-195 calls ReconstructData once per degraded read (one stripe

@@ -9,6 +9,7 @@
 // usage: rs_test [--cpu]   (--cpu: only the tests that need no GPU)
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -16,6 +17,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../blb_amd/host/client.hpp"
@@ -243,14 +245,25 @@ class memPieces : public client::TractserverTalker {
     std::map<std::string, Bytes> pieces;
     std::map<std::string, bool> down;
     std::atomic<int> reads{0};
-    std::pair<Bytes, Error> Read(const std::string& addr, core::TractID, int, int length, int64_t off) override {
+    std::map<std::string, bool> slow;      // blocks until its context is cancelled (or 20 s)
+    std::atomic<int> cancelled_reads{0};
+    std::pair<Bytes, Error> Read(const core::ContextPtr& ctx, const std::string& addr, core::TractID, int, int length,
+                                 int64_t off) override {
         ++reads;
-        if (down[addr]) return {Bytes(), Error::ErrRPC};
-        const Bytes& p = pieces[addr];
+        if (slow.count(addr) && slow.at(addr)) {
+            for (int i = 0; i < 20000 && !ctx->Done(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            if (ctx->Done()) {
+                ++cancelled_reads;
+                return {Bytes(), Error::ErrRPC};  // context canceled
+            }
+        }
+        if (down.count(addr) && down.at(addr)) return {Bytes(), Error::ErrRPC};
+        const Bytes& p = pieces.at(addr);
         const size_t end = std::min<size_t>(p.len(), off + length);
         return {Bytes::copy_of(p.data() + off, end - off), end == p.len() ? Error::ErrEOF : Error::NoError};
     }
-    std::pair<int, Error> ReadInto(const std::string& addr, core::TractID, int, Bytes b, int64_t off) override {
+    std::pair<int, Error> ReadInto(const core::ContextPtr&, const std::string& addr, core::TractID, int, Bytes b,
+                                   int64_t off) override {
         if (down[addr]) return {0, Error::ErrRPC};
         const Bytes& p = pieces[addr];
         const size_t n = std::min<size_t>(b.len(), p.len() - off);
@@ -298,7 +311,7 @@ static void TestClientRecovery(T* t) {
         std::memset(buf.data(), 0xEE, c.buf);
         client::TractPointer tc = tr;
         tc.Length = c.tractLen;
-        client::TractResult r = cli.readOneTractRS(tc, buf, c.off);
+        client::TractResult r = cli.readOneTractRS(core::Background(), tc, buf, c.off);
         if (r.err != c.err || r.read != c.want)
             Fatalf("read at %lld: %s, %d bytes", (long long)c.off, core::String(r.err), r.read);
         if (std::memcmp(buf.data(), sh[target].data() + c.off, c.want) != 0) Fatalf("wrong reconstructed bytes");
@@ -306,6 +319,111 @@ static void TestClientRecovery(T* t) {
             if (buf[i] != 0) Fatalf("not zero padded at %d", i);
     }
     if (cli.Reconstructs() != 3) Fatalf("want 3 reconstructs, got %d", cli.Reconstructs());
+}
+
+// reconstruct.go:119,154: once n good pieces are in, the straggler reads are cancelled
+// and the reconstruct returns without waiting for them.
+static void TestClientCancelsStragglers(T* t) {
+    const int n = 6, m = 3, target = 0;
+    const size_t S = 1 << 20;
+    std::mt19937_64 rng(4242);
+    auto [enc, e] = reedsolomon::New(n, m);
+    reedsolomon::Shards sh(n + m);
+    for (int i = 0; i < n; ++i) sh[i] = randBytes(rng, S);
+    for (int i = n; i < n + m; ++i) sh[i] = Bytes::make(S);
+    if (enc->Encode(sh) != reedsolomon::Err::None) Fatalf("encode");
+    memPieces ts;
+    client::TractPointer tr;
+    tr.Chunk = cid.Add(target);
+    tr.Host = "ts0";
+    tr.TSID = 100 + target;
+    tr.Length = static_cast<uint32_t>(S);
+    tr.Class = core::StorageClass::RS_6_3;
+    tr.BaseChunk = cid;
+    for (int i = 0; i < n + m; ++i) {
+        const std::string h = "ts" + std::to_string(i);
+        ts.pieces[h] = sh[i];
+        tr.OtherHosts.push_back(h);
+        tr.OtherTSIDs.push_back(100 + i);
+    }
+    ts.down["ts0"] = true;  // the piece we want
+    ts.slow["ts7"] = true;  // a straggler: 8 others are asked, 6 needed
+    ts.slow["ts8"] = true;
+    {
+        client::Client cli(&ts, client::ReconstructBehavior{});
+        Bytes buf = Bytes::make(S);
+        const auto t0 = std::chrono::steady_clock::now();
+        client::TractResult r = cli.readOneTractRS(core::Background(), tr, buf, 0);
+        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (r.err != Error::NoError || r.read != static_cast<int>(S)) Fatalf("read: %s, %d", core::String(r.err), r.read);
+        if (!buf.equal(sh[target])) Fatalf("wrong reconstructed bytes");
+        if (secs > 10.0) Fatalf("reconstruct waited for the stragglers (%.1f s)", secs);
+        for (int i = 0; i < 10000 && cli.OutstandingReads() > 0; ++i)
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        if (cli.OutstandingReads() != 0) Fatalf("straggler reads still running");
+    }
+    if (ts.cancelled_reads.load() != 2) Fatalf("want 2 cancelled straggler reads, got %d", ts.cancelled_reads.load());
+}
+
+// store.go:1029-1036: the increment loop stops at the first failing window.  A failing read
+// (here a short one: ErrVersionMismatch, store.go:1076-1077) must not be followed by any
+// read or write of a later window, pipelined or not.
+static void TestRSEncodeStopsAtFailingRead(T* t, bool pipeline) {
+    const int N = 3, M = 2, B = 12000;
+    memTractserverTalker tt;
+    tractserver::Store s(&tt, tractserver::Config{5000, pipeline});
+    auto addrs = makeAddrs(N + M);
+    std::mt19937_64 rng(7);
+    std::vector<Bytes> data(N);
+    for (int i = 0; i < N; ++i) data[i] = randBytes(rng, B);
+    const int cuts[4] = {0, 5000, 10000, 12000};
+    for (int w = 0; w < 3; ++w) {
+        for (int i = 0; i < N; ++i) {
+            Bytes b = data[i].slice(cuts[w], cuts[w + 1]);
+            if (w == 1 && i == 1) b = b.slice(0, b.len() - 1);  // short read in window 1
+            tt.addCtlReadReply(addrs[i].Host, b, Error::ErrEOF);
+        }
+        for (int i = N; i < N + M; ++i) tt.addCtlWriteReply(addrs[i].Host, Error::NoError);
+    }
+    std::vector<core::TSAddr> srcs(addrs.begin(), addrs.begin() + N), dests(addrs.begin() + N, addrs.end());
+    Error err = s.RSEncode(cid, B, srcs, dests, {});
+    if (err != Error::ErrVersionMismatch) Fatalf("want ErrVersionMismatch, got %s", core::String(err));
+    for (int i = 0; i < N; ++i)
+        if (tt.ctlReadCalls[addrs[i].Host] != 2) Fatalf("src %d: %d reads, want 2", i, tt.ctlReadCalls[addrs[i].Host]);
+    for (int i = N; i < N + M; ++i)
+        if (tt.ctlWriteCalls[addrs[i].Host].size() != 1) Fatalf("dest %d: %zu writes, want 1", i, tt.ctlWriteCalls[addrs[i].Host].size());
+}
+
+// A failing CtlWrite in window 1: no write of window 2 is ever sent.  Sequential: exactly
+// the reference's reads (windows 0 and 1); pipelined: window 2's reads may already have
+// been issued (documented difference; reads have no side effects).
+static void TestRSEncodeStopsAtFailingWrite(T* t, bool pipeline) {
+    const int N = 3, M = 2, B = 12000;
+    memTractserverTalker tt;
+    tractserver::Store s(&tt, tractserver::Config{5000, pipeline});
+    auto addrs = makeAddrs(N + M);
+    std::mt19937_64 rng(8);
+    std::vector<Bytes> data(N);
+    for (int i = 0; i < N; ++i) data[i] = randBytes(rng, B);
+    const int cuts[4] = {0, 5000, 10000, 12000};
+    for (int w = 0; w < 3; ++w) {
+        for (int i = 0; i < N; ++i) tt.addCtlReadReply(addrs[i].Host, data[i].slice(cuts[w], cuts[w + 1]), Error::ErrEOF);
+        tt.addCtlWriteReply(addrs[N].Host, w == 1 ? Error::ErrUnknown : Error::NoError);
+        tt.addCtlWriteReply(addrs[N + 1].Host, Error::NoError);
+    }
+    std::vector<core::TSAddr> srcs(addrs.begin(), addrs.begin() + N), dests(addrs.begin() + N, addrs.end());
+    Error err = s.RSEncode(cid, B, srcs, dests, {});
+    if (err != Error::ErrUnknown) Fatalf("want ErrUnknown, got %s", core::String(err));
+    for (int i = N; i < N + M; ++i) {
+        const auto& w = tt.ctlWriteCalls[addrs[i].Host];
+        if (w.size() != 2) Fatalf("dest %d: %zu writes, want 2", i, w.size());
+        for (const auto& x : w)
+            if (x.Off >= 10000) Fatalf("dest %d: write of window 2 sent", i);
+    }
+    for (int i = 0; i < N; ++i) {
+        const int r = tt.ctlReadCalls[addrs[i].Host];
+        if (pipeline ? (r < 2 || r > 3) : r != 2) Fatalf("src %d: %d reads", i, r);
+    }
 }
 
 int main(int argc, char** argv) {
@@ -321,6 +439,11 @@ int main(int argc, char** argv) {
         {"TestRSReconstruct/pipelined", [](T* t) { TestRSReconstruct(t, true); }, true},
         {"TestReconstructDataIntoCallerBuffer", TestReconstructDataIntoCallerBuffer, true},
         {"TestClientRecovery", TestClientRecovery, true},
+        {"TestClientCancelsStragglers", TestClientCancelsStragglers, true},
+        {"TestRSEncodeStopsAtFailingRead", [](T* t) { TestRSEncodeStopsAtFailingRead(t, false); }, true},
+        {"TestRSEncodeStopsAtFailingRead/pipelined", [](T* t) { TestRSEncodeStopsAtFailingRead(t, true); }, true},
+        {"TestRSEncodeStopsAtFailingWrite", [](T* t) { TestRSEncodeStopsAtFailingWrite(t, false); }, true},
+        {"TestRSEncodeStopsAtFailingWrite/pipelined", [](T* t) { TestRSEncodeStopsAtFailingWrite(t, true); }, true},
     };
     int failed = 0, ran = 0;
     for (const Test& tc : tests) {

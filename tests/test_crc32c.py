@@ -120,3 +120,33 @@ def test_oracle_crc32c_hw_equals_table(oracle_lib):
         blk = block or n
         assert np.array_equal(O.crc32c_blocks_hw(d, blk, threads=3), oracle_lib.crc32c_blocks(d, blk)), (n, blk)
     assert O.crc32c_blocks_hw(np.frombuffer(b"123456789", np.uint8), 9)[0] == CHECK
+
+
+@gpu
+def test_gpu_crc32c_at_phase_and_seeds(oracle_lib):
+    """blbrs_crc32c_dev_at: rows that are file windows starting `phase` bytes into a block,
+    block 0 continuing a seed (crc32.Update, checksum_block.go:80); streaming kernel (dword
+    phases and lengths) and segment kernel (odd phases, odd lengths, unaligned rows)."""
+    from blb_amd import checksum
+    torch = _torch()
+    O = oracle_lib
+    rng = np.random.default_rng(11)
+    cases = [(65532, 256, 4194304), (65532, 65528, 1 << 20), (65532, 4, 65532), (65532, 65000, 4096),
+             (65532, 1, 100003), (4096, 4092, 70000), (1000, 999, 12345), (65536, 12, 3 * 65536 + 8),
+             (65532, 513, 7), (1 << 20, 4, 3 << 20)]
+    for block, phase, n in cases:
+        for lead in (0, 3):
+            B = 3
+            base = torch.from_numpy(rng.integers(0, 256, (B, n + 16), dtype=np.uint8)).cuda()
+            rows = base[:, lead:lead + n]
+            seeds_h = rng.integers(0, 1 << 32, B, dtype=np.uint64).astype(np.uint32)
+            seeds = torch.from_numpy(seeds_h.view(np.int32)).cuda()
+            got = checksum.as_uint32(checksum.ChecksumBatch(rows, block, phase=phase, seeds=seeds))
+            host = rows.cpu().numpy()
+            for b in range(B):
+                want, pos, i = [], 0, 0
+                while pos < n:
+                    end = min(n, (i + 1) * block - phase)
+                    want.append(O.crc32c(host[b, pos:end], int(seeds_h[b]) if i == 0 else 0))
+                    pos, i = end, i + 1
+                assert np.array_equal(got[b], np.array(want, np.uint32)), (block, phase, n, lead, b)

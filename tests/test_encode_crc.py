@@ -109,3 +109,104 @@ def test_encode_crc_tile_grid_cases(oracle_lib):
             run_case(oracle_lib, k, m, S, block, B=B, pad=pad, seed=200 + i)
         finally:
             del os.environ["BLBRS_EC_PERSISTENT"]
+
+
+def _expected_blocks_at(O, buf, block, phase, seed):
+    """crc32.Update chain of a file window: buffer byte 0 sits `phase` bytes into block 0."""
+    out, pos, i = [], 0, 0
+    while pos < buf.size or (i == 0 and buf.size == 0):
+        end = min(buf.size, (i + 1) * block - phase)
+        out.append(O.crc32c(buf[pos:end], seed if i == 0 else 0))
+        pos, i = end, i + 1
+    return np.array(out, np.uint32)
+
+
+def test_encode_crc_piece_in_increment_windows(oracle_lib):
+    """rsEncodeOne's real schedule (store.go:1028-1037,1115): a 67,043,264-byte RS piece
+    (curator RSPieceLength) is encoded in EncodeIncrementSize = 4 MiB windows (the last one
+    4,128,704 bytes), each written at offset 4 MiB * i of the parity piece, whose receiver
+    checksums FILE-aligned 65532-byte ChecksumFile blocks and chains appends with crc32.Update
+    (pkg/disk/checksum_block.go:76-81).  Per window: EncodeBatchCRC(phase = offset mod 65532,
+    seed = the previous window's last, partial block CRC).  The per-window outputs, combined,
+    must equal the oracle's 65532-byte block CRCs of the whole parity piece; the same for
+    ChecksumBatch(phase, seeds) over the parity rows."""
+    from blb_amd import checksum
+    O = oracle_lib
+    k, m, B = 6, 3, 2
+    L, inc, blk = 67043264, 4 << 20, 65532
+    g = torch.Generator(device="cuda")
+    g.manual_seed(97531)
+    piece = torch.empty((B, k + m, L), dtype=torch.uint8, device="cuda")
+    piece[:, :k].random_(0, 256, generator=g)
+    piece[:, k:].fill_(0xEE)
+    enc = rs.New(k, m)
+    combined = [[[] for _ in range(B)] for _ in range(m)]
+    combined2 = [[[] for _ in range(B)] for _ in range(m)]
+    prev = prev2 = None
+    off = 0
+    while off < L:
+        ln = min(inc, L - off)
+        phase = off % blk
+        win = piece[:, :, off:off + ln]
+        seeds = prev if phase else None
+        crc = enc.EncodeBatchCRC(win, blk, phase=phase, seeds=seeds)
+        # the same windows through the plain CRC entry point, row by row
+        crc2 = torch.stack([checksum.ChecksumBatch(win[:, k + j], blk, phase=phase,
+                                                   seeds=None if not phase else prev2[j].contiguous())
+                            for j in range(m)])
+        assert tuple(crc.shape) == (m, B, (phase + ln + blk - 1) // blk)
+        last_partial = (off + ln) % blk != 0 and off + ln < L
+        for c, acc in ((crc, combined), (crc2, combined2)):
+            h = c.cpu().numpy().view(np.uint32)
+            for j in range(m):
+                for b in range(B):
+                    acc[j][b].extend(h[j, b, :-1] if last_partial else h[j, b])
+        prev = crc[:, :, -1].contiguous()
+        prev2 = crc2[:, :, -1]
+        off += ln
+    host = piece.cpu().numpy()
+    for b in range(B):
+        sh = [host[b, i] for i in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
+        O.encode(k, m, sh, use_avx2=True, threads=8)
+        for j in range(m):
+            assert np.array_equal(host[b, k + j], sh[k + j]), (b, j, "parity")
+            want = O.crc32c_blocks(sh[k + j], blk)
+            assert len(combined[j][b]) == want.size
+            assert np.array_equal(np.array(combined[j][b], np.uint32), want), (b, j, "fused")
+            assert np.array_equal(np.array(combined2[j][b], np.uint32), want), (b, j, "crc32c_dev_at")
+
+
+@pytest.mark.parametrize("k,m", [(6, 3), (10, 4), (5, 5), (12, 5)])
+def test_encode_crc_phase_and_seed_shapes(oracle_lib, k, m):
+    """Phase / seed on every path: the tile kernel (aligned phases, partial last tiles), the
+    2-pass fallback (k = 5, rows = 5, unaligned phases or lengths)."""
+    O = oracle_lib
+    rng = np.random.default_rng(k * 100 + m)
+    enc = rs.New(k, m)
+    cases = [(4128704, 65532, 256), (1 << 20, 65532, 65528), (200000, 4096, 4092), (8192 * 3 + 48, 8192, 4),
+             (70001, 65532, 1000), (65536, 65532, 65531), (4096, 65532, 65000), (16, 65532, 0), (1 << 20, 0, 0)]
+    for S, block, phase in cases:
+        B = 2
+        host = rng.integers(0, 256, (B, k + m, S), dtype=np.uint8)
+        host[:, k:] = 0x5A
+        dev = torch.from_numpy(host).cuda()
+        seeds_h = rng.integers(0, 1 << 32, (m, B), dtype=np.uint64).astype(np.uint32)
+        seeds = torch.from_numpy(seeds_h.view(np.int32)).cuda() if block else None
+        crc = enc.EncodeBatchCRC(dev, block, phase=phase, seeds=seeds).cpu().numpy().view(np.uint32)
+        got = dev.cpu().numpy()
+        blk = block or S
+        for b in range(B):
+            sh = [host[b, i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+            O.encode(k, m, sh, use_avx2=True, threads=8)
+            for j in range(m):
+                assert np.array_equal(got[b, k + j], sh[k + j]), (k, m, S, block, phase, b, j, "parity")
+                want = _expected_blocks_at(O, sh[k + j], blk, phase if block else 0,
+                                           int(seeds_h[j, b]) if block else 0)
+                assert np.array_equal(crc[j, b], want), (k, m, S, block, phase, b, j, "crc")
+
+
+def test_encode_crc_at_rejects_bad_phase():
+    enc = rs.New(6, 3)
+    st = torch.zeros((1, 9, 8192), dtype=torch.uint8, device="cuda")
+    with pytest.raises(rs.ErrInvalidArgument):
+        enc.EncodeBatchCRC(st, 65532, phase=65532)

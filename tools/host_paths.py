@@ -1,15 +1,20 @@
 """Measure the host-memory (PCIe-inclusive) paths on one MI355X:
   * raw pinned H2D / D2H / bidirectional copy rates (the ceiling);
-  * EncodeHostBatch (streaming, pinned) vs stream count;
+  * EncodeHostBatch of pinned stripes (zero-copy);
   * per-call Encode on pageable numpy shards at the tractserver's EncodeIncrementSize
     (4 MiB, internal/tractserver/config.go:117) and at a full 8 MiB tract, next to the CPU
-    oracle doing the same call.
+    oracle doing the same call;
+  * per-call Encode / ReconstructData on shards from the pinned buffer pool
+    (blbrs_buffer_get = rpc.GetBuffer, pkg/rpc/pool.go) from 1..16 concurrent threads, the
+    way concurrent RSEncode RPCs (internal/tractserver/store.go:1099) and degraded reads
+    (client/blb/reconstruct.go:173) call it.
 Prints one JSON object."""
 from __future__ import annotations
 
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -63,14 +68,12 @@ def main():
     host = pinned.numpy()
     host[:, :k] = np.random.default_rng(1).integers(0, 256, (nb, k, S), dtype=np.uint8)
     lists = [[host[b, i] for i in range(k + m)] for b in range(nb)]
-    res = {}
-    for ns in (1, 2, 3, 4, 6, 8):
-        enc.EncodeHostBatch(lists, nstreams=ns)
-        t = time.perf_counter()
-        enc.EncodeHostBatch(lists, nstreams=ns)
-        el = time.perf_counter() - t
-        res[ns] = round(nb * k * S / GIB / el, 2)
-    out["stream_encode_GiBps_data_by_nstreams"] = res
+    enc.EncodeHostBatch(lists)
+    t = time.perf_counter()
+    enc.EncodeHostBatch(lists)
+    el = time.perf_counter() - t
+    out["host_batch_encode_pinned_GiBps_data"] = round(nb * k * S / GIB / el, 2)
+    del lists, host, pinned
 
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS") or 16)
@@ -99,7 +102,56 @@ def main():
                                                    "gpu_pinned_GiBps": round(gpu_pin, 2),
                                                    "cpu_oracle_avx2_GiBps": round(cpu, 2),
                                                    "cpu_threads": threads}
+    out["pool_calls"] = pool_calls(k, m)
     print(json.dumps(out))
+
+
+def pool_calls(k, m):
+    """Per-call host Encode / ReconstructData of one stripe of 4 MiB pool buffers per call,
+    T threads each looping over its own stripe for ~2 s."""
+    res = {}
+    S = 4 * MIB
+    enc = rs.New(k, m, devices=[0])
+    for T in (1, 2, 4, 8, 16):
+        stripes = []
+        for t in range(T):
+            sh = [rs.GetBuffer(S) for _ in range(k + m)]
+            rng = np.random.default_rng(t)
+            for i in range(k):
+                sh[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+            enc.Encode(sh)
+            stripes.append(sh)
+        for op in ("encode", "reconstruct_data1"):
+            counts = [0] * T
+            stop = time.perf_counter() + 2.0
+
+            def loop(t):
+                sh = stripes[t]
+                out1 = sh[1]
+                while time.perf_counter() < stop:
+                    if op == "encode":
+                        enc.Encode(sh)
+                    else:
+                        work = list(sh)
+                        work[1] = None
+                        enc.ReconstructData(work, outs={1: out1})
+                    counts[t] += 1
+
+            t0 = time.perf_counter()
+            th = [threading.Thread(target=loop, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            el = time.perf_counter() - t0
+            res[f"{op}_T{T}_GiBps_data"] = round(sum(counts) * k * S / GIB / el, 2)
+            res[f"{op}_T{T}_calls_per_s"] = round(sum(counts) / el, 1)
+        for sh in stripes:
+            for b in sh:
+                rs.PutBuffer(b)
+    res["shard_bytes"] = S
+    res["device_stats"] = rs.device_stats(0)
+    return res
 
 
 if __name__ == "__main__":
