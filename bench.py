@@ -55,12 +55,20 @@ def parse():
     return p.parse_args()
 
 
+def lib_sha256():
+    import hashlib
+    from blb_amd import _lib
+    return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+
+
 def pmc_traffic(k, m, batch, shard):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary, if one exists for this
-    exact workload (profiles/pmc_*.json, written by tools/pmc_summary.py)."""
+    """HBM bytes per launch of the encode kernel from a committed rocprofv3 --pmc summary
+    (profiles/pmc_*.json, tools/pmc_prod.sh), used only when it was measured on THIS library
+    build (same libblbrs.so sha256) for this exact workload; else None."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
-        return None
+        return None, None
+    sha = lib_sha256()
     for fn in sorted(os.listdir(pdir), reverse=True):
         if fn.startswith("pmc_") and fn.endswith(".json"):
             try:
@@ -68,17 +76,29 @@ def pmc_traffic(k, m, batch, shard):
             except (OSError, ValueError):
                 continue
             w = d.get("workload", {})
-            if (w.get("k"), w.get("m"), w.get("batch"), w.get("shard")) == (k, m, batch, shard):
-                return d.get("hbm_bytes_per_launch")
-    return None
+            if (w.get("k"), w.get("m"), w.get("batch"), w.get("shard")) == (k, m, batch, shard) \
+                    and d.get("lib_sha256") == sha:
+                return d.get("hbm_bytes_per_launch"), fn
+    return None, None
 
 
 def cpu_baseline(k, m, seconds):
     """klauspost's algorithm (AVX2 vpshufb nibble tables, OpenMP byte-range split like
     codeSomeShardsP) from the oracle restatement, on a bounded sample of the workload."""
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    # Every core this process may run on (its affinity mask), capped by OMP_NUM_THREADS where
+    # the GPU box sets it to the job's CPU share.
+    affinity = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    threads = max(1, min(affinity, omp) if omp else affinity)
+    cpu_model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                cpu_model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     nstripes = 4
     rng = np.random.default_rng(97531)
     rows = O.build_matrix(k, m)[k:]
@@ -98,7 +118,8 @@ def cpu_baseline(k, m, seconds):
             break
     gibps = done * k * TRACT / GIB / el
     out = {"value": round(gibps, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-           "avx2": bool(O.lib().rso_have_avx2()),
+           "nproc": affinity, "os_cpu_count": os.cpu_count(), "omp_num_threads": omp or None,
+           "cpu_model": cpu_model, "avx2": bool(O.lib().rso_have_avx2()),
            "sample": f"RS({k},{m}) encode of {done} stripes x {k}x8MiB "
                      f"({done * k * TRACT / GIB:.1f} GiB data, {el:.1f} s) by the oracle's "
                      f"klauspost-AVX2 restatement, {threads} OpenMP threads"}
@@ -383,6 +404,7 @@ def main():
         cpu = cpu_baseline(k, m, a.cpu_seconds)
 
     if rank == 0:
+        traffic, traffic_src = pmc_traffic(k, m, B, S)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -406,7 +428,7 @@ def main():
                          "frac_vs_measured_copy": round(achieved_gbs / HBM_COPY_GBS, 4),
                          "kernel_ms": round(launch_ms, 3),
                          "algorithmic_bytes_per_launch": algo_bytes,
-                         "traffic": pmc_traffic(k, m, B, S)},
+                         "traffic": traffic, "traffic_source": traffic_src},
             "cpu_baseline": cpu,
             "verify_ok": ok,
         }

@@ -99,7 +99,8 @@ __device__ __forceinline__ uint32_t slice4(const LaneTabs& t, uint32_t x) {
 template <int LC>
 __device__ __forceinline__ uint32_t lane_piece(uint32_t lane) {
     if constexpr (LC == 64) return 16u * (4u * (lane & 15u) + (lane >> 4));
-    else return 16u * (2u * (lane & 31u) + (lane >> 5));
+    else if constexpr (LC == 32) return 16u * (2u * (lane & 31u) + (lane >> 5));
+    else return 16u * lane;  // LC 16: one piece per lane, already contiguous
 }
 
 // v[q][0..3] = this lane's piece of sub-row q -> v[i][0..3] = piece i of the lane's own
@@ -119,7 +120,7 @@ __device__ __forceinline__ void lane_contiguous(uint32_t (&v)[LC / 4]) {
             v[4 + d] = s01[1];
             v[8 + d] = s23[0];
             v[12 + d] = s23[1];
-        } else {
+        } else if constexpr (LC == 32) {
             auto s01 = __builtin_amdgcn_permlane32_swap(v[d], v[4 + d], false, false);
             v[d] = s01[0];
             v[4 + d] = s01[1];

@@ -48,14 +48,33 @@ constexpr uint64_t kOrd = 0x7FFFFFFFull;            // S_{kOrd} = I (checked on 
 #define BLBRS_ECT_COPIES 1
 #endif
 constexpr int kCopies = BLBRS_ECT_COPIES;           // interleaved copies of the slicing tables
+// Tuning builds only (tools/ect_variants.sh): 1 = skip the constant staging, 2 = skip the
+// slicing chains, 4 = skip the lane shifts.  Results are wrong with any bit set.
+#ifndef BLBRS_ECT_FLAGS
+#define BLBRS_ECT_FLAGS 0
+#endif
+constexpr int kFlags = BLBRS_ECT_FLAGS;
 
 // Shift matrices (v = 0: LC 64, v = 1: LC 32): lanemat[v][i][l] = column i of S_{LC*(63-l)}
 // (lane chunk end -> end of the wave's row; staged in LDS per workgroup, one conflict-free
 // column read per lane) and wavemat[v][w] = S_{64*LC*(3-w)} (row end -> tile end).
 struct TileConsts {
-    uint32_t lanemat[2][32][64];
-    uint32_t wavemat[2][4][32];
+    uint32_t lanemat[3][32][64];
+    uint32_t wavemat[3][4][32];
+    uint32_t tab8[8][256];  // slicing-by-8 tables: tab8[k][i] = CRC of byte i followed by k zeros
 };
+
+// Slicing-by-8 halves the chain's dependent LDS round trips (4 steps per 32-byte lane chunk
+// instead of 8; the second dword's lookups do not wait for the chain): RS(6,3) B=1024
+// 13.5-13.75 ms vs 13.7-13.95 ms for slicing-by-4 (tools/ect_ab.py, interleaved builds).
+#ifndef BLBRS_ECT_SLICE
+#define BLBRS_ECT_SLICE 8
+#endif
+constexpr int kSlice = BLBRS_ECT_SLICE;  // slicing-by-4 (CrcConsts tables) or -by-8 (tab8)
+#ifndef BLBRS_ECT_PREFETCH
+#define BLBRS_ECT_PREFETCH 1
+#endif
+constexpr bool kPrefetch = BLBRS_ECT_PREFETCH != 0;
 
 struct TArgs {
     const uint32_t* tables;
@@ -66,8 +85,10 @@ struct TArgs {
     uint64_t S, block, phase;
     const uint32_t* seeds;    // [j * B + b]: crc32.Update seed of block 0 (NULL = 0)
     uint32_t B, tps, xcd_remap, nblocks;
+    uint32_t tps_full;        // whole tiles per stripe (the main grid); tps - 1 when S % T != 0
     const CrcConsts* c;
     const uint32_t* lanemat;  // [32][64] for this LC
+    const uint32_t* tab8;     // [8][256]
     const uint32_t* wavemat;  // [4][32] for this LC
     uint32_t* raw;            // [(j * B + b) * tps + tile]: raw CRC of the tile's bytes
     uint32_t* hi;             // same index: raw CRC of the bytes past the tile's block boundary
@@ -75,7 +96,15 @@ struct TArgs {
 
 // 32-byte lane chunks for every shape: 8 KiB tiles, <= 165 VGPRs for rows <= 4 (3-4 waves per
 // SIMD); 64-byte chunks (16 KiB tiles, 2 waves per SIMD) measured slower.
-constexpr int lc_for(int, int) { return 32; }
+// 16-byte chunks (4 KiB tiles) for the widest shapes: half the input registers, twice the
+// lane shifts per byte.  RS(12,5) at 32-byte chunks needs 256 VGPRs (25.4 ms, B=512); at 16
+// it fits 94 (16.8 ms, the segment kernel's time, and it takes file phases).  RS(10,4) is
+// faster at 32 (11.4 vs 12.7 ms).
+#ifndef BLBRS_ECT_LC16_MIN
+#define BLBRS_ECT_LC16_MIN 17
+#endif
+constexpr int lc_for(int k, int rows) { return k + rows >= BLBRS_ECT_LC16_MIN ? 16 : 32; }
+constexpr int lc_index(int lc) { return lc == 64 ? 0 : lc == 32 ? 1 : 2; }
 
 // One slicing-by-4 step over C-copy tables (table 3-k serves byte k).
 template <int C>
@@ -89,96 +118,76 @@ __device__ __forceinline__ uint32_t slice4c(const uint32_t* tab, uint32_t copy, 
     return xor3(v[0], v[1], v[2]) ^ v[3];
 }
 
+// XOR over the 64 lanes, result in every lane, all on the VALU: DPP inside each 16-lane row
+// (swap neighbours, swap pairs, half-row mirror, row mirror), then permlane16/32 swaps across
+// rows -- no ds_bpermute through the LDS pipe the slicing lookups need.
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) v ^= __shfl_xor(v, s, 64);
-    return v;
+    v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
+    v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
+    v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0x141, 0xF, 0xF, false));  // half-row mirror
+    v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0x140, 0xF, 0xF, false));  // row mirror
+    auto r16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = r16[0] ^ r16[1];
+    auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return r32[0] ^ r32[1];
 }
 
-template <int K, int MR, int LC>
-__global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
+// o = S_{LC*(63-lane)} c per row (and the same for the hi chains when HI): the lane matrix's
+// 32 columns are read from LDS four at a time, one group ahead of the group being applied,
+// with scheduling fences in between -- without them the compiler hoists all 32 reads and
+// holds 32 registers through the whole CRC (which then no longer fits beside the next
+// tile's inputs).
+template <int MR>
+__device__ __forceinline__ void lane_shift(const uint32_t* lmat, uint32_t lane, const uint32_t (&crc)[MR],
+                                           uint32_t (&o)[MR]) {
+#pragma unroll
+    for (int j = 0; j < MR; ++j) o[j] = 0u;
+    uint32_t cur[4], nxt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = lmat[u * 64 + lane];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        if (g < 7) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) nxt[u] = lmat[((g + 1) * 4 + u) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = g * 4 + u;
+#pragma unroll
+            for (int j = 0; j < MR; ++j)
+                o[j] = __builtin_amdgcn_bitop3_b32(
+                    o[j], static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(crc[j]), i, 1)), cur[u], 0x78);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+    }
+}
+
+// One slicing-by-8 step: x = crc ^ first dword, y = second dword (byte k of x: table 7-k,
+// byte k of y: table 3-k).  The y lookups do not depend on the chain.
+__device__ __forceinline__ uint32_t slice8(const uint32_t* tab, uint32_t x, uint32_t y) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = tab[(7 - k) * 256 + __builtin_amdgcn_ubfe(x, 8 * k, 8)];
+        v[4 + k] = tab[(3 - k) * 256 + __builtin_amdgcn_ubfe(y, 8 * k, 8)];
+    }
+    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
+}
+
+// The CRC part of one tile: this lane's LC contiguous parity bytes per row (acc, already in
+// lane_contiguous order) -> raw / hi of the tile, written by threads 0..MR-1.  `red` is the
+// workgroup's reduction buffer for this tile (2 x 4 x MR words); one __syncthreads inside.
+template <int MR, int LC>
+__device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC / 4], const uint32_t* tab,
+                                         const uint32_t* lmat, uint32_t (*red)[4][MR], uint64_t tile_off,
+                                         uint64_t at0, uint32_t tid, uint32_t lane, uint32_t wave) {
     constexpr int NV = LC / 4;
-    constexpr int NQ = LC / 16;
     constexpr uint32_t kRow = 64u * LC;
     constexpr uint32_t kTile = 4u * kRow;
-    __shared__ uint32_t tab[4 * 256 * kCopies];
-    __shared__ uint32_t lmat[32 * 64];
-    __shared__ uint32_t red[2][4][MR];
-
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint32_t t = blockIdx.x;
-    if (a.xcd_remap) t = (t % 8u) * (gridDim.x / 8u) + t / 8u;
-    const uint32_t b = t / a.tps;
-    const uint32_t tile = t - b * a.tps;
-    const uint64_t tile_off = static_cast<uint64_t>(tile) * kTile;
-    uint8_t* stripe = a.base + static_cast<uint64_t>(b) * a.stripe_stride;
-    const uint32_t in_tile = wave * kRow + lane_piece<LC>(lane);  // tile offset of piece q = 0
-    const uint64_t my_off = tile_off + in_tile;
-    // Bytes of this tile inside the shard (kTile except in a partial last tile; uniform).
-    const uint32_t lim = static_cast<uint32_t>(a.S - tile_off < kTile ? a.S - tile_off : kTile);
-    const bool full = lim == kTile;
-    const ci32 in_idx = as_const(a.in_idx);
-    const ci32 out_idx = as_const(a.out_idx);
-
-    constexpr int kFill = 4 * 256 * kCopies / kTThreads;  // table words per thread
-    constexpr int kMFill = 32 * 64 / kTThreads;            // lane-matrix words per thread
-    uint32_t tv[kFill], mv[kMFill];
-    {
-        const uint32_t* src = &a.c->table[0][0];
-#pragma unroll
-        for (int r = 0; r < kFill; ++r) tv[r] = src[(tid + r * kTThreads) / kCopies];
-#pragma unroll
-        for (int r = 0; r < kMFill; ++r) mv[r] = a.lanemat[tid + r * kTThreads];
-    }
-    // All K inputs in flight (nontemporal: every byte is read once).
-    uint32_t x[K][NV];
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        const uint8_t* p = stripe + static_cast<uint64_t>(in_idx[c]) * a.shard_stride + my_off;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            u32x4 v = u32x4{0u, 0u, 0u, 0u};
-            if (full || in_tile + 1024u * q < lim) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q));
-            x[c][4 * q] = v.x;
-            x[c][4 * q + 1] = v.y;
-            x[c][4 * q + 2] = v.z;
-            x[c][4 * q + 3] = v.w;
-        }
-    }
-    // Slicing tables (L2 hits): written to LDS once their loads, issued before the data's,
-    // have landed -- the in-order vmcnt lets that wait skip the data loads.
-#pragma unroll
-    for (int r = 0; r < kFill; ++r) tab[tid + r * kTThreads] = tv[r];
-#pragma unroll
-    for (int r = 0; r < kMFill; ++r) lmat[tid + r * kTThreads] = mv[r];
-
-    uint32_t acc[MR][NV] = {};
-    {
-        cu32 tables = as_const(a.tables);
-        asm volatile("" : "+s"(tables));
-#pragma unroll
-        for (int c = 0; c + 1 < K; c += 2)
-            madd2<MR, NV>(Groups<NV>(x[c]), [&](int r) { return tables + (r * K + c) * 5; }, Groups<NV>(x[c + 1]),
-                          [&](int r) { return tables + (r * K + c + 1) * 5; }, acc, MR);
-        if constexpr (K & 1)
-            madd<MR, NV>(Groups<NV>(x[K - 1]), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, MR);
-    }
-#pragma unroll
-    for (int j = 0; j < MR; ++j) {
-        uint8_t* q = stripe + static_cast<uint64_t>(out_idx[j]) * a.shard_stride + my_off;
-#pragma unroll
-        for (int u = 0; u < NQ; ++u)
-            if (full || in_tile + 1024u * u < lim)
-                __builtin_nontemporal_store(
-                    u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
-                    reinterpret_cast<u32x4*>(q + 1024 * u));
-    }
-
-    // CRC of this lane's LC contiguous parity bytes (tile offset LC * tid) per row.
-#pragma unroll
-    for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
-    __syncthreads();  // tables
     const uint32_t copy = lane % kCopies;
     // The first block boundary after the tile start; inside the tile -> the bytes past it
     // get their own raw CRC (hi).  Only the wave whose row holds the boundary needs a masked
@@ -188,63 +197,56 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     const uint32_t o = split ? static_cast<uint32_t>(nb - tile_off) : kTile;
     const uint32_t o_wave = o / kRow;
     const uint32_t mine = LC * tid;
-    uint32_t crc[MR], chi[MR];
-#pragma unroll
-    for (int j = 0; j < MR; ++j) crc[j] = chi[j] = 0u;
-    if (split && wave == o_wave) {
-#pragma unroll
-        for (int d = 0; d < NV; ++d) {
-            const bool keep = mine + 4u * d >= o;
-#pragma unroll
-            for (int j = 0; j < MR; ++j) {
-                crc[j] = slice4c<kCopies>(tab, copy, crc[j] ^ acc[j][d]);
-                chi[j] = slice4c<kCopies>(tab, copy, chi[j] ^ (keep ? acc[j][d] : 0u));
-            }
-        }
-    } else {
-#pragma unroll
-        for (int d = 0; d < NV; ++d)
-#pragma unroll
-            for (int j = 0; j < MR; ++j) crc[j] = slice4c<kCopies>(tab, copy, crc[j] ^ acc[j][d]);
-    }
-
-    // Shift each lane's chain to its row end (S_{LC*(63-lane)} from LDS) and XOR over the
-    // wave; the row -> tile-end shift is applied once per row in the final reduction.
+    // Pass 0: every byte (raw).  Pass 1, only in the wave whose row holds the boundary: the
+    // bytes past it (hi).  One code path for both keeps the register footprint of the rare
+    // split wave at that of the others.
     uint32_t o_raw[MR], o_hi[MR];
+    const uint32_t passes = split && wave == o_wave ? 2u : 1u;
+#pragma unroll 1
+    for (uint32_t pass = 0; pass < passes; ++pass) {
+        uint32_t crc[MR];
 #pragma unroll
-    for (int j = 0; j < MR; ++j) o_raw[j] = o_hi[j] = 0u;
-    if (split && wave == o_wave) {
+        for (int j = 0; j < MR; ++j) crc[j] = 0u;
+        if constexpr (kSlice == 8 && !(kFlags & 2)) {
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            const uint32_t col = lmat[i * 64 + lane];
+            for (int d = 0; d < NV; d += 2) {
+                const bool keep0 = pass == 0 || mine + 4u * d >= o;
+                const bool keep1 = pass == 0 || mine + 4u * d + 4u >= o;
 #pragma unroll
-            for (int j = 0; j < MR; ++j) {
-                o_raw[j] = __builtin_amdgcn_bitop3_b32(
-                    o_raw[j], static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(crc[j]), i, 1)), col, 0x78);
-                o_hi[j] = __builtin_amdgcn_bitop3_b32(
-                    o_hi[j], static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(chi[j]), i, 1)), col, 0x78);
+                for (int j = 0; j < MR; ++j)
+                    crc[j] = slice8(tab, crc[j] ^ (keep0 ? acc[j][d] : 0u), keep1 ? acc[j][d + 1] : 0u);
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < NV; ++d) {
+                const bool keep = pass == 0 || mine + 4u * d >= o;
+#pragma unroll
+                for (int j = 0; j < MR; ++j) {
+                    const uint32_t w = keep ? acc[j][d] : 0u;
+                    if constexpr (kFlags & 2) crc[j] ^= w;
+                    else crc[j] = slice4c<kCopies>(tab, copy, crc[j] ^ w);
+                }
             }
         }
+        // Shift each lane's chain to its row end (S_{LC*(63-lane)} from LDS) and XOR over the
+        // wave; the row -> tile-end shift is applied once per row in the final reduction.
+        uint32_t v[MR];
+        if constexpr (kFlags & 4) {
 #pragma unroll
-        for (int j = 0; j < MR; ++j) {
-            o_raw[j] = wave_xor(o_raw[j]);
-            o_hi[j] = wave_xor(o_hi[j]);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            const uint32_t col = lmat[i * 64 + lane];
-#pragma unroll
-            for (int j = 0; j < MR; ++j)
-                o_raw[j] = __builtin_amdgcn_bitop3_b32(
-                    o_raw[j], static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(crc[j]), i, 1)), col, 0x78);
+            for (int jj = 0; jj < MR; ++jj) v[jj] = crc[jj];
+        } else {
+            lane_shift<MR>(lmat, lane, crc, v);
         }
 #pragma unroll
-        for (int j = 0; j < MR; ++j) {
-            o_raw[j] = wave_xor(o_raw[j]);
-            o_hi[j] = split && wave > o_wave ? o_raw[j] : 0u;
+        for (int jj = 0; jj < MR; ++jj) {
+            v[jj] = wave_xor(v[jj]);
+            if (pass == 0) o_raw[jj] = v[jj];
+            else o_hi[jj] = v[jj];
         }
     }
+    if (passes == 1)
+#pragma unroll
+        for (int jj = 0; jj < MR; ++jj) o_hi[jj] = split && wave > o_wave ? o_raw[jj] : 0u;
     if (lane == 0)
 #pragma unroll
         for (int j = 0; j < MR; ++j) {
@@ -261,9 +263,130 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
             r ^= apply(wm + 32 * w, red[0][w][j]);
             h ^= apply(wm + 32 * w, red[1][w][j]);
         }
-        const uint64_t at = (static_cast<uint64_t>(j) * a.B + b) * a.tps + tile;
+        const uint64_t at = at0 + static_cast<uint64_t>(j) * a.B * a.tps;
         a.raw[at] = r;
         a.hi[at] = h;
+    }
+}
+
+// One workgroup streams NT consecutive tiles of one stripe (PARTIAL: its partial last tile,
+// NT = 1, in a second tiny launch so that the masking never touches the main kernel).  The
+// slicing tables and lane matrices are staged once per workgroup, and tile t+1's loads are
+// issued into the registers the multiply of tile t has just freed, before tile t's CRC: the
+// CRC of one tile runs under the next tile's loads instead of idling the workgroup's memory
+// pipe.  sched_barrier keeps that order (left alone the compiler hoists the loads over the
+// multiply, into fresh registers).
+template <int K, int MR, int LC, bool PARTIAL, int NT>
+__global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
+    constexpr int NV = LC / 4;
+    constexpr int NQ = LC / 16;
+    constexpr uint32_t kRow = 64u * LC;
+    constexpr uint32_t kTile = 4u * kRow;
+    __shared__ uint32_t tab[kSlice * 256 * kCopies];
+    __shared__ uint32_t lmat[32 * 64];
+    __shared__ uint32_t red[2][2][4][MR];
+
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t b, first, count;
+    if constexpr (PARTIAL) {
+        b = blockIdx.x;
+        first = a.tps - 1;
+        count = 1;
+    } else {
+        const uint32_t gps = (a.tps_full + NT - 1) / NT;  // tile groups per stripe
+        uint32_t t = blockIdx.x;
+        if (a.xcd_remap) t = (t % 8u) * (gridDim.x / 8u) + t / 8u;
+        b = t / gps;
+        first = (t - b * gps) * NT;
+        count = a.tps_full - first < static_cast<uint32_t>(NT) ? a.tps_full - first : NT;
+    }
+    uint8_t* stripe = a.base + static_cast<uint64_t>(b) * a.stripe_stride;
+    const uint32_t in_tile = wave * kRow + lane_piece<LC>(lane);  // tile offset of piece q = 0
+    // Bytes of the partial tile inside the shard (a multiple of 16).
+    const uint32_t lim = PARTIAL ? static_cast<uint32_t>(a.S - static_cast<uint64_t>(first) * kTile) : kTile;
+    const ci32 in_idx = as_const(a.in_idx);
+    const ci32 out_idx = as_const(a.out_idx);
+
+    constexpr int kFill = kSlice * 256 * kCopies / kTThreads;  // table words per thread
+    constexpr int kMFill = 32 * 64 / kTThreads;            // lane-matrix words per thread
+    uint32_t tv[kFill], mv[kMFill];
+    if constexpr (kFlags & 1) {
+#pragma unroll
+        for (int r = 0; r < kFill; ++r) tv[r] = tid * 3u + r;
+#pragma unroll
+        for (int r = 0; r < kMFill; ++r) mv[r] = tid * 5u + r;
+    } else {
+        const uint32_t* src = kSlice == 8 ? a.tab8 : &a.c->table[0][0];
+#pragma unroll
+        for (int r = 0; r < kFill; ++r) tv[r] = src[(tid + r * kTThreads) / kCopies];
+#pragma unroll
+        for (int r = 0; r < kMFill; ++r) mv[r] = a.lanemat[tid + r * kTThreads];
+    }
+    // All K inputs of a tile in flight (nontemporal: every byte is read once).
+    uint32_t x[K][NV];
+    auto load_tile = [&](uint64_t tile_off) {
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const uint8_t* p = stripe + static_cast<uint64_t>(in_idx[c]) * a.shard_stride + tile_off + in_tile;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                u32x4 v = u32x4{0u, 0u, 0u, 0u};
+                if (!PARTIAL || in_tile + 1024u * q < lim)
+                    v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q));
+                x[c][4 * q] = v.x;
+                x[c][4 * q + 1] = v.y;
+                x[c][4 * q + 2] = v.z;
+                x[c][4 * q + 3] = v.w;
+            }
+        }
+    };
+    load_tile(static_cast<uint64_t>(first) * kTile);
+    // Slicing tables (L2 hits): written to LDS once their loads, issued before the data's,
+    // have landed -- the in-order vmcnt lets that wait skip the data loads.
+#pragma unroll
+    for (int r = 0; r < kFill; ++r) tab[tid + r * kTThreads] = tv[r];
+#pragma unroll
+    for (int r = 0; r < kMFill; ++r) lmat[tid + r * kTThreads] = mv[r];
+
+#pragma unroll 1
+    for (uint32_t i = 0; i < count; ++i) {
+        const uint32_t tile = first + i;
+        const uint64_t tile_off = static_cast<uint64_t>(tile) * kTile;
+        if constexpr (NT > 1 && !kPrefetch)
+            if (i > 0) load_tile(tile_off);
+        uint32_t acc[MR][NV] = {};
+        {
+            cu32 tables = as_const(a.tables);
+            asm volatile("" : "+s"(tables));
+#pragma unroll
+            for (int c = 0; c + 1 < K; c += 2)
+                madd2<MR, NV>(Groups<NV>(x[c]), [&](int r) { return tables + (r * K + c) * 5; }, Groups<NV>(x[c + 1]),
+                              [&](int r) { return tables + (r * K + c + 1) * 5; }, acc, MR);
+            if constexpr (K & 1)
+                madd<MR, NV>(Groups<NV>(x[K - 1]), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, MR);
+        }
+#pragma unroll
+        for (int j = 0; j < MR; ++j) {
+            uint8_t* q = stripe + static_cast<uint64_t>(out_idx[j]) * a.shard_stride + tile_off + in_tile;
+#pragma unroll
+            for (int u = 0; u < NQ; ++u)
+                if (!PARTIAL || in_tile + 1024u * u < lim)
+                    __builtin_nontemporal_store(
+                        u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
+                        reinterpret_cast<u32x4*>(q + 1024 * u));
+        }
+        if constexpr (NT > 1 && kPrefetch) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (i + 1 < count) load_tile(tile_off + kTile);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // CRC of this lane's LC contiguous parity bytes (tile offset LC * tid) per row.
+#pragma unroll
+        for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
+        if (i == 0) __syncthreads();  // tables
+        crc_tile<MR, LC>(a, acc, tab, lmat, red[i & 1], tile_off, static_cast<uint64_t>(b) * a.tps + tile, tid, lane,
+                         wave);
     }
 }
 
@@ -301,27 +424,36 @@ __global__ __launch_bounds__(256) void tile_combine_kernel(TArgs a, uint32_t log
 
 using KernelFn = void (*)(TArgs);
 
-template <int K>
+// Tiles per workgroup in the main launch.  1: a loop over several tiles (staging amortised,
+// the next tile's loads issued before this tile's CRC) holds 149 VGPRs for RS(6,3) -> 3 waves
+// per SIMD, and measured 5-7 % slower than one tile per workgroup at 111 VGPRs / 4 waves.
+#ifndef BLBRS_ECT_NT
+#define BLBRS_ECT_NT 1
+#endif
+constexpr int kTilesPerGroup = BLBRS_ECT_NT;
+
+template <int K, bool P>
 KernelFn pick_rows(int rows) {
-    constexpr int LC = lc_for(K, 0);
+    constexpr int NT = P ? 1 : kTilesPerGroup;
     switch (rows) {
-        case 1: return encode_crc_tile_kernel<K, 1, LC>;
-        case 2: return encode_crc_tile_kernel<K, 2, LC>;
-        case 3: return encode_crc_tile_kernel<K, 3, LC>;
-        case 4: return encode_crc_tile_kernel<K, 4, LC>;
-        default: return nullptr;  // rows = 5 spills here; the segment kernel is faster (§4e)
+        case 1: return encode_crc_tile_kernel<K, 1, lc_for(K, 1), P, NT>;
+        case 2: return encode_crc_tile_kernel<K, 2, lc_for(K, 2), P, NT>;
+        case 3: return encode_crc_tile_kernel<K, 3, lc_for(K, 3), P, NT>;
+        case 4: return encode_crc_tile_kernel<K, 4, lc_for(K, 4), P, NT>;
+        case 5: return encode_crc_tile_kernel<K, 5, lc_for(K, 5), P, NT>;
+        default: return nullptr;
     }
 }
 
 // Same instantiated shapes as encode_crc.hip (blb's classes, RS(10,4), RS(3,2), RS(4,2)).
-KernelFn pick(int k, int rows) {
+KernelFn pick(int k, int rows, bool partial = false) {
     switch (k) {
-        case 3: return pick_rows<3>(rows);
-        case 4: return pick_rows<4>(rows);
-        case 6: return pick_rows<6>(rows);
-        case 8: return pick_rows<8>(rows);
-        case 10: return pick_rows<10>(rows);
-        case 12: return pick_rows<12>(rows);
+        case 3: return partial ? pick_rows<3, true>(rows) : pick_rows<3, false>(rows);
+        case 4: return partial ? pick_rows<4, true>(rows) : pick_rows<4, false>(rows);
+        case 6: return partial ? pick_rows<6, true>(rows) : pick_rows<6, false>(rows);
+        case 8: return partial ? pick_rows<8, true>(rows) : pick_rows<8, false>(rows);
+        case 10: return partial ? pick_rows<10, true>(rows) : pick_rows<10, false>(rows);
+        case 12: return partial ? pick_rows<12, true>(rows) : pick_rows<12, false>(rows);
         default: return nullptr;
     }
 }
@@ -337,8 +469,16 @@ hipError_t tile_consts_for(const TileConsts** out) {
     auto& slot = g_consts[dev];
     if (!slot) {
         static TileConsts host;  // built under g_mu
-        for (int v = 0; v < 2; ++v) {
-            const uint64_t lc = v == 0 ? 64 : 32;
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t v = i;
+            for (int j = 0; j < 8; ++j) v = (v & 1u) ? (v >> 1) ^ kCrcPoly : v >> 1;
+            host.tab8[0][i] = v;
+        }
+        for (int k = 1; k < 8; ++k)
+            for (uint32_t i = 0; i < 256; ++i)
+                host.tab8[k][i] = (host.tab8[k - 1][i] >> 8) ^ host.tab8[0][host.tab8[k - 1][i] & 255u];
+        for (int v = 0; v < 3; ++v) {
+            const uint64_t lc = v == 0 ? 64 : v == 1 ? 32 : 16;
             uint32_t col[32];
             for (int l = 0; l < 64; ++l) {
                 crc_shift_matrix(lc * static_cast<uint64_t>(63 - l), col);
@@ -410,21 +550,28 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     a.block = in.block < in.S + in.phase ? in.block : in.S + in.phase;
     a.seeds = in.seeds;
     a.B = in.B;
-    const uint32_t log2t = lc == 64 ? 14u : 13u;
+    const uint32_t log2t = lc == 64 ? 14u : lc == 32 ? 13u : 12u;
     a.tps = static_cast<uint32_t>((in.S + (uint64_t{1} << log2t) - 1) >> log2t);
+    a.tps_full = static_cast<uint32_t>(in.S >> log2t);
     a.nblocks = static_cast<uint32_t>((in.S + a.phase + a.block - 1) / a.block);
     a.c = c;
-    a.lanemat = &tc->lanemat[lc == 64 ? 0 : 1][0][0];
-    a.wavemat = &tc->wavemat[lc == 64 ? 0 : 1][0][0];
+    a.lanemat = &tc->lanemat[lc_index(lc)][0][0];
+    a.wavemat = &tc->wavemat[lc_index(lc)][0][0];
+    a.tab8 = &tc->tab8[0][0];
     const uint64_t tiles = static_cast<uint64_t>(in.B) * a.tps;
-    a.xcd_remap = tiles % 8 == 0 ? 1u : 0u;
+    const uint64_t groups = static_cast<uint64_t>(in.B) * ((a.tps_full + kTilesPerGroup - 1) / kTilesPerGroup);
+    a.xcd_remap = groups % 8 == 0 ? 1u : 0u;
     const uint64_t nraw = static_cast<uint64_t>(in.rows) * tiles;
     uint32_t* buf = nullptr;
     if ((e = hipMallocAsync(reinterpret_cast<void**>(&buf), nraw * 8, stream)) != hipSuccess) return e;
     a.raw = buf;
     a.hi = buf + nraw;
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(tiles)), dim3(kTThreads), 0, stream, a);
+    if (groups) hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), 0, stream, a);
     e = hipGetLastError();
+    if (e == hipSuccess && a.tps != a.tps_full) {
+        hipLaunchKernelGGL(pick(in.k, in.rows, true), dim3(in.B), dim3(kTThreads), 0, stream, a);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) {
         const uint64_t total = static_cast<uint64_t>(in.rows) * in.B * a.nblocks;
         hipLaunchKernelGGL(tile_combine_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,

@@ -51,5 +51,9 @@ for rep in range(a.reps):
                 for key in env:
                     del os.environ[key]
             res.setdefault(f"{name}_{blk_name}", []).append(ms)
+    # file-aligned window (rsEncodeOne's parity window at 4 MiB: phase 256) with seeds
+    seeds = torch.zeros((m, B), dtype=torch.int32, device=dev)
+    res.setdefault("tile_b65532_phase256_seeded", []).append(
+        timed(lambda: enc.EncodeBatchCRC(stripes, 65532, phase=256, seeds=seeds)))
 out = {key: [round(v, 3) for v in vals] for key, vals in res.items()}
 print(json.dumps({"k": k, "m": m, "B": B, "ms": out}))

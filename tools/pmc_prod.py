@@ -1,0 +1,51 @@
+"""PMC driver for the PRODUCTION library (blb_amd/libblbrs.so as bench.py loads it), run under
+`rocprofv3 --pmc ...` by tools/pmc_prod.sh.  One dispatch of each hot-path kernel at the
+BASELINE size, plus calibration kernels of known traffic in the same process:
+
+  calib_copy      torch copy_ of 8 GiB (reads 8 GiB, writes 8 GiB)
+  encode          EncodeBatch, RS(6,3) B=1024 x 8 MiB          (rs_code_kernel, store)
+  reconstruct     ReconstructBatch, data shard 1 missing        (rs_code_kernel, 1 row)
+  verify          VerifyBatch                                   (rs_code_kernel, verify)
+  encode_crc      EncodeBatchCRC(65532)                         (encode_crc_tile_kernel + combine)
+
+Markers: the dispatch order is fixed; tools/pmc_prod_summary.py matches kernels by name and
+order.  Prints the libblbrs.so sha256 it loaded."""
+import hashlib
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from blb_amd import _lib  # noqa: E402
+from blb_amd import reedsolomon as rs  # noqa: E402
+
+k, m, B, S = 6, 3, 1024, 8 << 20
+dev = torch.device("cuda:0")
+src = torch.empty(8 << 30, dtype=torch.uint8, device=dev)
+dst = torch.empty_like(src)
+src.fill_(1)
+torch.cuda.synchronize()
+dst.copy_(src)  # calib_copy
+torch.cuda.synchronize()
+del src, dst
+torch.cuda.empty_cache()
+st = torch.empty((B, k + m, S), dtype=torch.uint8, device=dev)
+g = torch.Generator(device=dev)
+g.manual_seed(97531)
+st[:, :k].random_(0, 256, generator=g)
+enc = rs.New(k, m)
+torch.cuda.synchronize()
+enc.EncodeBatch(st)
+torch.cuda.synchronize()
+enc.ReconstructBatch(st, [i != 1 for i in range(k + m)], data_only=True)
+torch.cuda.synchronize()
+ok = enc.VerifyBatch(st)
+torch.cuda.synchronize()
+crc = enc.EncodeBatchCRC(st, 65532)
+torch.cuda.synchronize()
+lib = _lib.LIB_PATH
+print(json.dumps({"lib": lib, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+                  "verify_ok": bool(ok.all()), "k": k, "m": m, "batch": B, "shard": S}))
