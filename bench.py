@@ -394,6 +394,25 @@ def main():
         extra["pack_tracts"] = {"hbm_GBps": round(pk_bytes / (pk_ms * 1e-3) / 1e9, 1), "ms": round(pk_ms, 3),
                                 "pieces": B * k, "tracts": sum(len(e) for e in per_col),
                                 "bytes_read": read_bytes, "bytes_written": B * k * S}
+        # PackTracts fused with Encode (curator encPack -> encEncode in one pass): the same
+        # extents as data shard j of stripe b = piece b*k + j; parity encoded from registers.
+        fused_ext = sorted(((src, off, ln, b * k + j) for j in range(k) for (src, off, ln, b) in per_col[j]),
+                           key=lambda x: (x[3], x[1]))
+        pack.PackEncode(enc, stripes, fused_ext)
+        torch.cuda.synchronize(dev)
+        fe_evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        torch.cuda._sleep(400_000_000)
+        fe_evs[0].record(stream)
+        pack.PackEncode(enc, stripes, fused_ext)
+        fe_evs[1].record(stream)
+        torch.cuda.synchronize(dev)
+        fe_ms = fe_evs[0].elapsed_time(fe_evs[1])
+        fe_ok = bool(enc.VerifyBatch(stripes).all())
+        fe_bytes = read_bytes + B * (k + m) * S
+        extra["pack_encode_fused"] = {"ms": round(fe_ms, 3), "hbm_GBps": round(fe_bytes / (fe_ms * 1e-3) / 1e9, 1),
+                                      "separate_pack_plus_encode_ms": round(pk_ms + launch_ms, 3),
+                                      "bytes_read": read_bytes, "bytes_written": B * (k + m) * S,
+                                      "verify_ok": fe_ok, "kernel": "pack_encode_kernel"}
         del pool, per_col
 
     if not a.no_extra and a.shard == TRACT:

@@ -38,6 +38,7 @@ SIGNATURES = {
     "blbrs_crc32c_dev_at": (_I, [_P, _SZ, _SZ, _SZ, _SZ, _SZ, _P, _P, _P]),
     "blbrs_encode_crc_dev_at": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _SZ, _SZ, _P, _P, _P]),
     "blbrs_pack_dev": (_I, [_P, _SZ, _SZ, _SZ, _P, _SZ, _P]),
+    "blbrs_pack_encode_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P, _SZ, _P]),
     "blbrs_batcher_new": (_I, [_I, _I, ctypes.POINTER(_P)]),
     "blbrs_batcher_free": (None, [_P]),
     "blbrs_encoder_set_batcher": (_I, [_P, _P]),

@@ -1352,22 +1352,12 @@ int blbrs_encoder_set_batcher(blbrs_encoder* enc, blbrs_batcher* b) {
 
 // ---- PackTracts ----
 
-int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece_len,
-                   const blbrs_pack_extent* extents, size_t nextents, void* stream) {
-    if (npieces == 0 || piece_len == 0) {
-        if (nextents) return fail(BLBRS_ERR_INVALID_ARG, "extents given for empty pieces");
-        return BLBRS_OK;
-    }
-    if (!dst || (nextents && !extents)) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
-    if (npieces > 1 && dst_stride < piece_len) return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than piece length");
-    DevCall dc;
-    int rc = dc.enter(dst);
-    if (rc) return rc;
-    uint64_t dview = 0;
-    if (!rt::device_view(dst, &dview)) return fail(BLBRS_ERR_INVALID_ARG, "pack destination is not device-accessible");
-    // checkTractSpec (store.go:996-1009) per piece, plus the table: piece starts, then
-    // {src, offset, length, piece} per extent.
-    std::vector<uint64_t> table(npieces + 1 + 4 * nextents);
+// checkTractSpec (store.go:996-1009) per piece, plus the device table: piece starts, then
+// {src (device view), offset, length, piece} per extent.
+static int build_pack_table(size_t npieces, size_t piece_len, const blbrs_pack_extent* extents, size_t nextents,
+                            std::vector<uint64_t>* out) {
+    std::vector<uint64_t>& table = *out;
+    table.assign(npieces + 1 + 4 * nextents, 0);
     uint64_t* ex = table.data() + npieces + 1;
     size_t next_piece = 0;
     uint64_t end = 0;
@@ -1401,6 +1391,24 @@ int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece
         ex[4 * i + 3] = x.piece;
     }
     while (next_piece <= npieces) table[next_piece++] = nextents;
+    return BLBRS_OK;
+}
+
+int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece_len,
+                   const blbrs_pack_extent* extents, size_t nextents, void* stream) {
+    if (npieces == 0 || piece_len == 0) {
+        if (nextents) return fail(BLBRS_ERR_INVALID_ARG, "extents given for empty pieces");
+        return BLBRS_OK;
+    }
+    if (!dst || (nextents && !extents)) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (npieces > 1 && dst_stride < piece_len) return fail(BLBRS_ERR_INVALID_ARG, "stride smaller than piece length");
+    DevCall dc;
+    int rc = dc.enter(dst);
+    if (rc) return rc;
+    uint64_t dview = 0;
+    if (!rt::device_view(dst, &dview)) return fail(BLBRS_ERR_INVALID_ARG, "pack destination is not device-accessible");
+    std::vector<uint64_t> table;
+    if ((rc = build_pack_table(npieces, piece_len, extents, nextents, &table))) return rc;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     rt::PtrLease lease;
     const uint64_t* tdev = nullptr;
@@ -1409,6 +1417,58 @@ int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece
     hipError_t e = pack_pieces(reinterpret_cast<uint8_t*>(dview), dst_stride, npieces, piece_len, tdev, s);
     if (e != hipSuccess) return hip_fail(e, "pack_pieces");
     return BLBRS_OK;
+}
+
+int blbrs_pack_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                          size_t batch, size_t shard_len, const blbrs_pack_extent* extents, size_t nextents,
+                          void* stream) {
+    if (!enc) return fail(BLBRS_ERR_INVALID_ARG, "enc is NULL");
+    if (batch == 0 || shard_len == 0) {
+        if (nextents) return fail(BLBRS_ERR_INVALID_ARG, "extents given for empty pieces");
+        return BLBRS_OK;
+    }
+    if (nextents && !extents) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (batch > 0x7FFFFFFFull) return fail(BLBRS_ERR_INVALID_ARG, "batch too large");
+    Stripes st;
+    int rc = dev_stripes_strided(stripes, shard_stride, stripe_stride, batch, shard_len, &st);
+    if (rc) return rc;
+    DevCall dc;
+    if ((rc = dc.enter(stripes))) return rc;
+    const size_t npieces = batch * static_cast<size_t>(enc->k);
+    std::vector<uint64_t> table;
+    if ((rc = build_pack_table(npieces, shard_len, extents, nextents, &table))) return rc;
+    auto hp = enc->encode_plan();
+    const DevPlan* plan = nullptr;
+    if ((rc = enc->dev_plan("E", *hp, dc.dev, &plan))) return rc;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    rt::PtrLease lease;
+    const uint64_t* tdev = nullptr;
+    bool unused = false;
+    if ((rc = lease.upload(table.data(), table.size(), s, &tdev, &unused))) return rc;
+    if (plan->passes.size() == 1) {
+        PackEncodeArgs a{};
+        a.tables = plan->passes[0].tables;
+        a.out_idx = plan->passes[0].out_idx;
+        a.base = stripes;
+        a.shard_stride = shard_stride;
+        a.stripe_stride = stripe_stride;
+        a.S = shard_len;
+        a.B = static_cast<uint32_t>(batch);
+        a.k = static_cast<uint32_t>(enc->k);
+        a.rows = static_cast<uint32_t>(plan->passes[0].rows);
+        a.table = tdev;
+        a.nextents = nextents;
+        if (pack_encode_supported(a)) {
+            const hipError_t e = launch_pack_encode(a, s);
+            if (e != hipSuccess) return hip_fail(e, "launch pack_encode_kernel");
+            return BLBRS_OK;
+        }
+    }
+    // No fused instantiation: PackTracts into the data shards, then Encode (same bytes).
+    hipError_t e = pack_pieces(stripes, shard_stride, npieces, shard_len, tdev, s, static_cast<uint32_t>(enc->k),
+                               stripe_stride);
+    if (e != hipSuccess) return hip_fail(e, "pack_pieces");
+    return run_plan(*plan, st, batch, shard_len, Mode::kStore, nullptr, s);
 }
 
 // ---- pinned host memory ----

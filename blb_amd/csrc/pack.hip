@@ -20,6 +20,8 @@ struct PackArgs {
     uint64_t dst_stride, piece_len;
     uint32_t npieces, tiles_per_piece;
     const uint64_t* table;
+    uint32_t per_group;    // pieces per group: piece p at dst + (p / per_group) * group_stride
+    uint64_t group_stride; //   + (p % per_group) * dst_stride
 };
 
 constexpr int kUnroll = 4;
@@ -119,7 +121,8 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
             n = half;
         }
     }
-    uint8_t* d = a.dst + piece * a.dst_stride;
+    uint8_t* d = a.dst + static_cast<uint64_t>(piece / a.per_group) * a.group_stride +
+                 static_cast<uint64_t>(piece % a.per_group) * a.dst_stride;
     uint64_t cur = t0;
     for (uint64_t e = lo; cur < t1;) {
         const uint64_t off = e < hi ? ex[4 * e + 1] : t1;
@@ -140,11 +143,16 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
 }  // namespace
 
 hipError_t pack_pieces(uint8_t* dst, uint64_t dst_stride, uint64_t npieces, uint64_t piece_len,
-                       const uint64_t* table_dev, hipStream_t stream) {
+                       const uint64_t* table_dev, hipStream_t stream, uint32_t per_group, uint64_t group_stride) {
     if (npieces == 0 || piece_len == 0) return hipSuccess;
     const uint64_t tpp = (piece_len + kPackTile - 1) / kPackTile;
     if (npieces > 0xFFFFFFFFull || tpp * npieces > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    PackArgs a{dst, dst_stride, piece_len, static_cast<uint32_t>(npieces), static_cast<uint32_t>(tpp), table_dev};
+    if (per_group == 0) {
+        per_group = 1;
+        group_stride = dst_stride;
+    }
+    PackArgs a{dst, dst_stride, piece_len, static_cast<uint32_t>(npieces), static_cast<uint32_t>(tpp), table_dev,
+               per_group, group_stride};
     hipLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(tpp * npieces)), dim3(kPackThreads), 0, stream, a);
     return hipGetLastError();
 }

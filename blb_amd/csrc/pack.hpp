@@ -16,8 +16,29 @@ namespace blbrs {
 constexpr uint32_t kPackTile = 64u * 1024u;  // destination bytes per workgroup
 constexpr int kPackThreads = 256;
 
-// Piece p is written at dst + p * dst_stride, piece_len bytes.  Asynchronous on `stream`.
+// Piece p is written at dst + p * dst_stride, piece_len bytes (per_group > 0: at
+// dst + (p / per_group) * group_stride + (p % per_group) * dst_stride -- data shard j of
+// stripe b for per_group = k).  Asynchronous on `stream`.
 hipError_t pack_pieces(uint8_t* dst, uint64_t dst_stride, uint64_t npieces, uint64_t piece_len,
-                       const uint64_t* table_dev, hipStream_t stream);
+                       const uint64_t* table_dev, hipStream_t stream, uint32_t per_group = 0,
+                       uint64_t group_stride = 0);
+
+// PackTracts fused with Encode (pack_encode.hip): the k data shards of each of B strided
+// stripes are assembled from the extent table (piece b * k + j = data shard j of stripe b,
+// same table layout as above) and, in the same pass, the m parity shards are encoded from
+// the assembled bytes -- the data pieces are written once and never read back.
+struct PackEncodeArgs {
+    const uint32_t* tables;   // device: encode pass v_perm tables [rows][k][5]
+    const int32_t* out_idx;   // device: [rows] parity shard indices
+    uint8_t* base;            // shard i of stripe b at base + b * stripe_stride + i * shard_stride
+    uint64_t shard_stride, stripe_stride, S;
+    uint32_t B, k, rows;
+    const uint64_t* table;    // device extent table (pieces = B * k)
+    uint64_t nextents;        // extents in the table
+};
+// True when a fused instantiation covers the shape (k in blb's list, rows <= 5, 16-byte
+// aligned base and strides); otherwise the caller packs, then encodes.
+bool pack_encode_supported(const PackEncodeArgs& a);
+hipError_t launch_pack_encode(const PackEncodeArgs& a, hipStream_t stream);
 
 }  // namespace blbrs

@@ -118,3 +118,21 @@ def PackPieces(dst, piece_len: int, extents: Sequence[tuple], stream=None) -> No
         s = _torch_stream(dst) if dst.is_cuda else torch.cuda.current_stream().cuda_stream
     _check(_lib.load().blbrs_pack_dev(dst.data_ptr(), dst.stride(0), npieces, piece_len,
                                      ex.ctypes.data if len(ex) else None, len(ex), s))
+
+
+def PackEncode(enc, stripes, extents: Sequence[tuple], stream=None) -> None:
+    """PackTracts fused with Encode (blbrs_pack_encode_dev): for each stripe b of a
+    [B, k+m, S] CUDA tensor, data shard j is assembled from the extents of piece b*k + j
+    (same (src, offset, length, piece) tuples as PackPieces, piece_len = S) and the m parity
+    shards are encoded from it -- one pass over HBM.  Asynchronous on `stream`."""
+    B, S, ss, bs = enc._stripes(stripes)
+    ex = np.zeros(len(extents), EXTENT_DTYPE)
+    for i, (src, off, ln, piece) in enumerate(extents):
+        if off < 0 or ln < 0 or piece < 0:
+            raise ErrInvalidArgument(f"extent {i}: negative field")
+        if _is_torch(src) and src.numel() < ln:
+            raise ErrInvalidArgument(f"extent {i}: source shorter than its length")
+        ex[i] = (_addr(src) if ln else 0, off, ln, piece)
+    s = stream if stream is not None else _torch_stream(stripes)
+    _check(_lib.load().blbrs_pack_encode_dev(enc._h, stripes.data_ptr(), ss, bs, B, S,
+                                            ex.ctypes.data if len(ex) else None, len(ex), s))

@@ -302,6 +302,18 @@ typedef struct {
 int blbrs_pack_dev(uint8_t* dst, size_t dst_stride, size_t npieces, size_t piece_len,
                    const blbrs_pack_extent* extents, size_t nextents, void* stream);
 
+/* PackTracts fused with Encode: the curator's encPack then encEncode
+ * (internal/curator/pack_tracts.go:244-292; Store.PackTracts store.go:922-994, then
+ * Encoder.Encode store.go:1099) in ONE pass over HBM.  For each of `batch` strided stripes
+ * (layout as blbrs_encode_dev), data shard j of stripe b is the packed piece number
+ * b * k + j of `extents` (same rules as blbrs_pack_dev, piece_len = shard_len: tracts at
+ * their offsets, zero elsewhere), and parity shards k..k+m-1 are its encoding.  The data
+ * bytes are written once and never read back.  Same results as blbrs_pack_dev over the data
+ * shards followed by blbrs_encode_dev (which is what shapes without a fused kernel run). */
+int blbrs_pack_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
+                          size_t stripe_stride, size_t batch, size_t shard_len,
+                          const blbrs_pack_extent* extents, size_t nextents, void* stream);
+
 /* ---- misc ---- */
 int blbrs_set_device(int device);      /* hipSetDevice for the calling thread (the library
                                           itself never relies on it) */

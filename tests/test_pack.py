@@ -221,3 +221,77 @@ def test_gpu_pack_then_encode_matches_oracle():
     par = N.encode(k, m, [d[:65536] for d in data])  # sampled columns: oracle is pure numpy
     for j in range(m):
         assert np.array_equal(got[k + j, :65536], par[j]), j
+
+
+def _long_extents(rng, npieces, piece_len, pool_len):
+    """Multi-MiB tracts at padToLength multiples (the packer's layout): most tiles lie inside
+    one extent (the fused kernel's COPY path) with every source misalignment."""
+    ext = []
+    for p in range(npieces):
+        off = 0
+        while True:
+            ln = int(rng.integers(1, min(piece_len, 3 << 20) + 1))
+            if off + ln > piece_len:
+                break
+            src = int(rng.integers(0, pool_len - ln + 1))
+            ext.append((src, off, ln, p))
+            off += pack.padded_length(ln)
+    return ext
+
+
+@gpu
+@pytest.mark.parametrize("k,m,S,layout", [(6, 3, 8 << 20, "long"), (6, 3, 1_000_003, "short"),
+                                          (10, 4, 4 << 20, "long"), (12, 5, 65537, "short"),
+                                          (3, 2, 20000, "short"), (5, 5, 70001, "short"),
+                                          (6, 3, 4096, "long"), (8, 3, 3 << 20, "long")])
+def test_gpu_pack_encode_fused_vs_oracle(oracle_lib, k, m, S, layout):
+    """blbrs_pack_encode_dev: data shards == oracle pack_piece (tracts at offsets, zero
+    holes and pad) and parity == oracle encode of those pieces; stale bytes everywhere
+    before the call; (5,5) has no fused instantiation and runs pack then encode."""
+    torch = _torch()
+    from blb_amd import reedsolomon
+    rng = np.random.default_rng(S + 7 * k + m)
+    B = 3
+    pool = rng.integers(0, 256, 12 << 20, dtype=np.uint8)
+    dpool = torch.from_numpy(pool).cuda()
+    mk = _long_extents if layout == "long" else _random_extents
+    ext = mk(rng, B * k, S, pool.size)
+    st = torch.full((B, k + m, S), 0xEE, dtype=torch.uint8, device="cuda")
+    enc = reedsolomon.New(k, m)
+    pack.PackEncode(enc, st, [(dpool[s:], off, ln, p) for s, off, ln, p in ext])
+    got = st.cpu().numpy()
+    for b in range(B):
+        data = []
+        for j in range(k):
+            p = b * k + j
+            want = N.pack_piece(S, [(pool[s:s + ln].tobytes(), off) for s, off, ln, q in ext if q == p])
+            want = np.frombuffer(want.ljust(S, b"\0"), np.uint8)
+            assert np.array_equal(got[b, j], want), (b, j, "data")
+            data.append(want.copy())
+        sh = data + [np.zeros(S, np.uint8) for _ in range(m)]
+        oracle_lib.encode(k, m, sh, use_avx2=True, threads=8)
+        for j in range(m):
+            assert np.array_equal(got[b, k + j], sh[k + j]), (b, j, "parity")
+
+
+@gpu
+def test_gpu_pack_encode_equals_pack_then_encode():
+    """The fused call equals PackPieces over the data shards followed by EncodeBatch, at the
+    BASELINE tract size."""
+    torch = _torch()
+    from blb_amd import reedsolomon
+    rng = np.random.default_rng(5)
+    k, m, B, S = 6, 3, 8, 8 << 20
+    dpool = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device="cuda")
+    ext = _long_extents(rng, B * k, S, dpool.numel())
+    a = torch.full((B, k + m, S), 0x33, dtype=torch.uint8, device="cuda")
+    b = a.clone()
+    enc = reedsolomon.New(k, m)
+    pack.PackEncode(enc, a, [(dpool[s:], off, ln, p) for s, off, ln, p in ext])
+    flat = b.view(B * (k + m), S)
+    rows = torch.arange(B * (k + m), device="cuda").view(B, k + m)[:, :k].reshape(-1)
+    tmp = torch.empty((B * k, S), dtype=torch.uint8, device="cuda")
+    pack.PackPieces(tmp, S, [(dpool[s:], off, ln, p) for s, off, ln, p in ext])
+    flat[rows] = tmp
+    enc.EncodeBatch(b)
+    assert torch.equal(a, b)
