@@ -62,7 +62,12 @@ struct TileConsts {
     uint32_t lanemat[3][32][64];
     uint32_t wavemat[3][4][32];
     uint32_t tab8[8][256];  // slicing-by-8 tables: tab8[k][i] = CRC of byte i followed by k zeros
+    // Nibble tables of the lane shifts, two factors: S_{LC*(63-l)} = A_{(63-l)>>3} B_{(63-l)&7}
+    // with B_b = S_{LC*b} (tables 0..7) and A_a = S_{8*LC*a} (tables 8..15); table t, nibble
+    // k, value v at [t * kNibStride + 16 * k + v] = the matrix applied to v << 4k.
+    uint32_t nib[3][16 * 136];
 };
+constexpr uint32_t kNibStride = 136;  // 128 + 8 words: the 16 tables start on 8 different banks
 
 // Slicing-by-8 halves the chain's dependent LDS round trips (4 steps per 32-byte lane chunk
 // instead of 8; the second dword's lookups do not wait for the chain): RS(6,3) B=1024
@@ -166,6 +171,32 @@ __device__ __forceinline__ void lane_shift(const uint32_t* lmat, uint32_t lane, 
     }
 }
 
+// Lane shifts by nibble tables (default) or by 32 columns: RS(12,5) 15.99 vs 16.32 ms,
+// RS(10,4) 11.02 vs 11.11, RS(6,3) 13.11 vs 13.10 (tools/ect_ab.py, profiles/r02/ect_ab/r2n).
+#ifndef BLBRS_ECT_NIB
+#define BLBRS_ECT_NIB 1
+#endif
+constexpr bool kNib = BLBRS_ECT_NIB != 0;
+
+__device__ __forceinline__ uint32_t apply_nib(const uint32_t* t, uint32_t c) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = t[16 * k + __builtin_amdgcn_ubfe(c, 4 * k, 4)];
+    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
+}
+
+// o = S_{LC*(63-lane)} c per row through two nibble-table factors (16 LDS lookups and ~40
+// VALU per value instead of 32 columns x 2 VALU).
+template <int MR>
+__device__ __forceinline__ void lane_shift_nib(const uint32_t* nt, uint32_t lane, const uint32_t (&crc)[MR],
+                                               uint32_t (&o)[MR]) {
+    const uint32_t e = 63u - lane;
+    const uint32_t* tb = nt + (e & 7u) * kNibStride;
+    const uint32_t* ta = nt + (8u + (e >> 3)) * kNibStride;
+#pragma unroll
+    for (int j = 0; j < MR; ++j) o[j] = apply_nib(ta, apply_nib(tb, crc[j]));
+}
+
 // One slicing-by-8 step: x = crc ^ first dword, y = second dword (byte k of x: table 7-k,
 // byte k of y: table 3-k).  The y lookups do not depend on the chain.
 __device__ __forceinline__ uint32_t slice8(const uint32_t* tab, uint32_t x, uint32_t y) {
@@ -183,7 +214,7 @@ __device__ __forceinline__ uint32_t slice8(const uint32_t* tab, uint32_t x, uint
 // workgroup's reduction buffer for this tile (2 x 4 x MR words); one __syncthreads inside.
 template <int MR, int LC>
 __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC / 4], const uint32_t* tab,
-                                         const uint32_t* lmat, uint32_t (*red)[4][MR], uint64_t tile_off,
+                                         const uint32_t* lmat, const uint32_t* wm, uint32_t (*red)[4][MR], uint64_t tile_off,
                                          uint64_t at0, uint32_t tid, uint32_t lane, uint32_t wave) {
     constexpr int NV = LC / 4;
     constexpr uint32_t kRow = 64u * LC;
@@ -234,6 +265,8 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
         if constexpr (kFlags & 4) {
 #pragma unroll
             for (int jj = 0; jj < MR; ++jj) v[jj] = crc[jj];
+        } else if constexpr (kNib) {
+            lane_shift_nib<MR>(lmat, lane, crc, v);
         } else {
             lane_shift<MR>(lmat, lane, crc, v);
         }
@@ -254,18 +287,32 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
             red[1][wave][j] = o_hi[j];
         }
     __syncthreads();
-    if (tid < MR) {
-        const uint32_t j = tid;
-        const cu32 wm = as_const(a.wavemat);
-        uint32_t r = red[0][3][j], h = red[1][3][j];
+    // Row ends -> tile end, spread over lanes: wave 0 folds the raw values, wave 1 the hi
+    // values; lane 8j + s takes half s&1 of S_{64*LC*(3-w)} (w = s>>1, 16 columns) on row j's
+    // wave-w value (s = 6: wave 3's value unshifted, s = 7: nothing), and the 8-lane group
+    // XORs -- 32 VALU per lane instead of six serial 32-column applies in one wave.
+    if (wave < 2 && lane < 8u * MR) {
+        const uint32_t j = lane >> 3, sl = lane & 7u;
+        uint32_t t = 0u;
+        if (sl < 6u) {
+            const uint32_t w = sl >> 1, h16 = (sl & 1u) * 16u;
+            const uint32_t v = red[wave][w][j];
+            const uint32_t* col = wm + 32u * w + h16;
 #pragma unroll
-        for (int w = 0; w < 3; ++w) {
-            r ^= apply(wm + 32 * w, red[0][w][j]);
-            h ^= apply(wm + 32 * w, red[1][w][j]);
+            for (int i = 0; i < 16; ++i)
+                t = __builtin_amdgcn_bitop3_b32(
+                    t, static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(v), static_cast<int>(h16) + i, 1)),
+                    col[i], 0x78);
+        } else if (sl == 6u) {
+            t = red[wave][3][j];
         }
-        const uint64_t at = at0 + static_cast<uint64_t>(j) * a.B * a.tps;
-        a.raw[at] = r;
-        a.hi[at] = h;
+        t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
+        t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
+        t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0x141, 0xF, 0xF, false));  // half-row mirror
+        if (sl == 0u) {
+            const uint64_t at = at0 + static_cast<uint64_t>(j) * a.B * a.tps;
+            (wave == 0 ? a.raw : a.hi)[at] = t;
+        }
     }
 }
 
@@ -283,8 +330,9 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     constexpr uint32_t kRow = 64u * LC;
     constexpr uint32_t kTile = 4u * kRow;
     __shared__ uint32_t tab[kSlice * 256 * kCopies];
-    __shared__ uint32_t lmat[32 * 64];
+    __shared__ uint32_t lmat[kNib ? 16 * kNibStride : 32 * 64];
     __shared__ uint32_t red[2][2][4][MR];
+    __shared__ uint32_t wm[96];  // S_{64*LC*(3-w)}, w < 3
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -309,7 +357,8 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     const ci32 out_idx = as_const(a.out_idx);
 
     constexpr int kFill = kSlice * 256 * kCopies / kTThreads;  // table words per thread
-    constexpr int kMFill = 32 * 64 / kTThreads;            // lane-matrix words per thread
+    constexpr int kMWords = kNib ? 16 * kNibStride : 32 * 64;
+    constexpr int kMFill = (kMWords + kTThreads - 1) / kTThreads;  // lane-shift words per thread
     uint32_t tv[kFill], mv[kMFill];
     if constexpr (kFlags & 1) {
 #pragma unroll
@@ -321,8 +370,12 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
 #pragma unroll
         for (int r = 0; r < kFill; ++r) tv[r] = src[(tid + r * kTThreads) / kCopies];
 #pragma unroll
-        for (int r = 0; r < kMFill; ++r) mv[r] = a.lanemat[tid + r * kTThreads];
+        for (int r = 0; r < kMFill; ++r) {
+            const uint32_t i = tid + r * kTThreads;
+            mv[r] = (kMWords % kTThreads == 0 || i < kMWords) ? a.lanemat[i] : 0u;
+        }
     }
+    const uint32_t wmv = tid < 96u ? a.wavemat[tid] : 0u;
     // All K inputs of a tile in flight (nontemporal: every byte is read once).
     uint32_t x[K][NV];
     auto load_tile = [&](uint64_t tile_off) {
@@ -347,7 +400,11 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
 #pragma unroll
     for (int r = 0; r < kFill; ++r) tab[tid + r * kTThreads] = tv[r];
 #pragma unroll
-    for (int r = 0; r < kMFill; ++r) lmat[tid + r * kTThreads] = mv[r];
+    for (int r = 0; r < kMFill; ++r) {
+        const uint32_t i = tid + r * kTThreads;
+        if (kMWords % kTThreads == 0 || i < kMWords) lmat[i] = mv[r];
+    }
+    if (tid < 96u) wm[tid] = wmv;
 
 #pragma unroll 1
     for (uint32_t i = 0; i < count; ++i) {
@@ -385,7 +442,7 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
 #pragma unroll
         for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
         if (i == 0) __syncthreads();  // tables
-        crc_tile<MR, LC>(a, acc, tab, lmat, red[i & 1], tile_off, static_cast<uint64_t>(b) * a.tps + tile, tid, lane,
+        crc_tile<MR, LC>(a, acc, tab, lmat, wm, red[i & 1], tile_off, static_cast<uint64_t>(b) * a.tps + tile, tid, lane,
                          wave);
     }
 }
@@ -488,6 +545,16 @@ hipError_t tile_consts_for(const TileConsts** out) {
                 crc_shift_matrix(64 * lc * static_cast<uint64_t>(3 - w), col);
                 for (int i = 0; i < 32; ++i) host.wavemat[v][w][i] = col[i];
             }
+            for (int t = 0; t < 16; ++t) {
+                crc_shift_matrix(t < 8 ? lc * static_cast<uint64_t>(t) : 8 * lc * static_cast<uint64_t>(t - 8), col);
+                for (int k = 0; k < 8; ++k)
+                    for (uint32_t x = 0; x < 16; ++x) {
+                        uint32_t o = 0;
+                        for (int bit = 0; bit < 4; ++bit)
+                            if ((x >> bit) & 1u) o ^= col[4 * k + bit];
+                        host.nib[v][t * kNibStride + 16 * k + x] = o;
+                    }
+            }
         }
         TileConsts* d = nullptr;
         if ((e = hipMalloc(&d, sizeof(TileConsts))) != hipSuccess) return e;
@@ -555,7 +622,7 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     a.tps_full = static_cast<uint32_t>(in.S >> log2t);
     a.nblocks = static_cast<uint32_t>((in.S + a.phase + a.block - 1) / a.block);
     a.c = c;
-    a.lanemat = &tc->lanemat[lc_index(lc)][0][0];
+    a.lanemat = kNib ? &tc->nib[lc_index(lc)][0] : &tc->lanemat[lc_index(lc)][0][0];
     a.wavemat = &tc->wavemat[lc_index(lc)][0][0];
     a.tab8 = &tc->tab8[0][0];
     const uint64_t tiles = static_cast<uint64_t>(in.B) * a.tps;
