@@ -267,6 +267,9 @@ def main():
     local = local % max(1, torch.cuda.device_count())  # identity on a node with >= N GPUs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # One process per GPU: this rank's host-memory calls (config 5) stay on its own GPU
+    # instead of spreading over every visible device (the library's in-process default).
+    rs.set_default_devices([local])
     dist = None
     if world > 1:
         import torch.distributed as dist
