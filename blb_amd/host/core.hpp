@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace core {
 
@@ -24,6 +25,7 @@ enum class Error {
     ErrRPC,
     ErrUnknown,
     ErrAllocHost,
+    ErrNoSuchTract,
 };
 
 inline const char* String(Error e) {
@@ -38,6 +40,7 @@ inline const char* String(Error e) {
         case Error::ErrRPC: return "rpc error";
         case Error::ErrUnknown: return "unknown error";
         case Error::ErrAllocHost: return "could not allocate host";
+        case Error::ErrNoSuchTract: return "no such tract";
     }
     return "?";
 }
@@ -46,7 +49,21 @@ struct TractID {
     uint64_t Blob = 0;
     uint16_t Index = 0;
     bool operator==(const TractID& o) const { return Blob == o.Blob && Index == o.Index; }
+    bool operator<(const TractID& o) const { return Blob != o.Blob ? Blob < o.Blob : Index < o.Index; }
+    // ids.go:237-239: a valid regular blob (partition type 0, key > 0) or any blob of a
+    // valid RS partition (type 2).
+    bool IsValid() const {
+        const uint32_t p = static_cast<uint32_t>(Blob >> 32);
+        const bool part = (p & 0x3fffffffu) != 0;
+        return (part && (p >> 30) == 0 && static_cast<uint32_t>(Blob) > 0) || (part && (p >> 30) == 2);
+    }
 };
+
+// ids.go:196-198, 242-244
+inline uint64_t BlobIDFromParts(uint32_t partition, uint32_t key) {
+    return (static_cast<uint64_t>(partition) << 32) | key;
+}
+inline TractID TractIDFromParts(uint64_t blob, uint16_t index) { return TractID{blob, index}; }
 
 // ids.go:113 -- RS partitions have upper two bits 10.
 struct RSChunkID {
@@ -75,6 +92,16 @@ inline ContextPtr Background() { return std::make_shared<Context>(); }
 struct TSAddr {
     uint64_t ID = 0;
     std::string Host;
+};
+
+// core.PackTractSpec (internal/core/types.go): tract ID at Offset of the packed piece,
+// pulled from any of From.
+struct PackTractSpec {
+    TractID ID;
+    std::vector<TSAddr> From;
+    int Version = 0;
+    int Offset = 0;
+    int Length = 0;
 };
 
 // internal/core/StorageClass.go:7-13 and storageclass.go RSParams.

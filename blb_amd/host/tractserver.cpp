@@ -4,6 +4,7 @@
 #include "rpc.hpp"
 
 #include <algorithm>
+#include <cstring>
 #include <future>
 #include <thread>
 
@@ -14,6 +15,63 @@ using core::Error;
 // store.go:1132-1142 -- Reconstruct then Verify, fused into one device round trip.
 reedsolomon::Err reconstructAndVerify(reedsolomon::Encoder& enc, reedsolomon::Shards& data, bool* verified) {
     return enc.ReconstructAndVerify(data, verified);
+}
+
+bool checkTractSpec(const std::vector<core::PackTractSpec>& srcs, int length) {
+    int end = 0;
+    for (const auto& src : srcs) {
+        if (!src.ID.IsValid() || src.From.empty() || src.Offset < end) return false;
+        end = src.Offset + src.Length;
+    }
+    return length >= end;
+}
+
+Error Store::PackTracts(int length, const std::vector<core::PackTractSpec>& srcs, core::RSChunkID dest) {
+    if (!dest.IsValid() || !checkTractSpec(srcs, length)) return Error::ErrInvalidArgument;
+    const core::TractID destTract = dest.ToTractID();
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        tracts_.erase(destTract);  // removeTract
+    }
+    // The file ends at `length` when there are sources (the pad, store.go:974-980) and is
+    // empty otherwise.  Its bytes come from the pinned pool (not zeroed), so every hole is
+    // written explicitly, as the sparse file reads them: zeros.
+    const size_t size = srcs.empty() ? 0 : static_cast<size_t>(length);
+    blb::Bytes piece = size ? rpc::GetBuffer(size) : blb::Bytes::make(0);
+    size_t cursor = 0;
+    for (const auto& src : srcs) {
+        bool pulled = false;
+        for (const auto& from : src.From) {
+            // Ask for TractLength and compare with src.Length, so that a tract of an
+            // unexpected length is caught (store.go:953-962).
+            auto [b, err] = tt_->CtlRead(from.Host, src.ID, src.Version, static_cast<int>(core::TractLength), 0);
+            if ((err == Error::NoError || err == Error::ErrEOF) && static_cast<int>(b.len()) == src.Length) {
+                std::memset(piece.data() + cursor, 0, static_cast<size_t>(src.Offset) - cursor);
+                if (src.Length) std::memcpy(piece.data() + src.Offset, b.data(), static_cast<size_t>(src.Length));
+                cursor = static_cast<size_t>(src.Offset + src.Length);
+                pulled = true;
+                break;
+            }
+        }
+        if (!pulled) return Error::ErrRPC;  // the half-written file is deleted
+    }
+    if (size > cursor) std::memset(piece.data() + cursor, 0, size - cursor);
+    std::lock_guard<std::mutex> g(mu_);
+    tracts_[destTract] = Local{piece, core::RSChunkVersion};
+    return Error::NoError;
+}
+
+std::pair<blb::Bytes, Error> Store::Read(core::TractID id, int version, int length, int64_t off) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = tracts_.find(id);
+    if (it == tracts_.end()) return {blb::Bytes(), Error::ErrNoSuchTract};
+    if (it->second.version != version) return {blb::Bytes(), Error::ErrVersionMismatch};
+    const blb::Bytes& d = it->second.data;
+    const size_t start = std::min(static_cast<size_t>(std::max<int64_t>(off, 0)), d.len());
+    const size_t n = std::min(static_cast<size_t>(std::max(length, 0)), d.len() - start);
+    blb::Bytes out = rpc::GetBuffer(n);
+    if (n) std::memcpy(out.data(), d.data() + start, n);
+    return {out, static_cast<int>(n) < length ? Error::ErrEOF : Error::NoError};
 }
 
 Error Store::RSEncode(core::RSChunkID baseid, int length, const std::vector<core::TSAddr>& srcs,

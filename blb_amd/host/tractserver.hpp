@@ -2,7 +2,9 @@
 // Store::RSEncode / rsEncodeOne / reconstructAndVerify (internal/tractserver/store.go:1012-1144).
 #pragma once
 #include <cstdint>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "bytes.hpp"
@@ -37,6 +39,15 @@ class Store {
     core::Error RSEncode(core::RSChunkID baseid, int length, const std::vector<core::TSAddr>& srcs,
                          const std::vector<core::TSAddr>& dests, const std::vector<int>& indexMap);
 
+    // store.go:921-994 -- pull every source tract (sequentially, from the first replica that
+    // returns exactly src.Length bytes) into a local RS data piece of `length` bytes: tracts
+    // at their offsets, holes and the tail zero.  ErrInvalidArgument for a bad dest or spec,
+    // ErrRPC when a source cannot be pulled (nothing is kept).
+    core::Error PackTracts(int length, const std::vector<core::PackTractSpec>& srcs, core::RSChunkID dest);
+
+    // Store.Read of a local tract: [off, off + length) of it; a short read is ErrEOF.
+    std::pair<blb::Bytes, core::Error> Read(core::TractID id, int version, int length, int64_t off);
+
  private:
     struct Window {
         int64_t offset;
@@ -55,7 +66,17 @@ class Store {
 
     TractserverTalker* tt_;
     Config cfg_;
+    struct Local {
+        blb::Bytes data;  // pinned pool memory: the GPU codes it in place when read for RSEncode
+        int version;
+    };
+    std::mutex mu_;
+    std::map<core::TractID, Local> tracts_;
 };
+
+// store.go:998-1009: sources in order, non-overlapping, each from >= 1 host with a valid ID,
+// all inside `length`.
+bool checkTractSpec(const std::vector<core::PackTractSpec>& srcs, int length);
 
 // store.go:1132-1142; false with Err::None means errVerifyFailed.
 reedsolomon::Err reconstructAndVerify(reedsolomon::Encoder& enc, reedsolomon::Shards& data, bool* verified);

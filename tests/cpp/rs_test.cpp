@@ -1,5 +1,10 @@
 // rs_test.cpp -- blb's RS tests, ported to the C++ mirror over the MI355X engine.
 //
+// TestPackTractsInvalid / TestPackTractsRPCError / TestPackTracts follow
+// store_test.go:647-746 (golden bytes of the packed piece included); TestPackThenRSEncode
+// runs the curator's encPack -> encEncode flow (internal/curator/pack_tracts.go:244-292):
+// three data tractservers pack tracts into their pieces, a fourth RSEncodes them.
+//
 // TestRSEncode / TestRSReconstruct follow internal/tractserver/store_test.go:749-879 line
 // for line (memTractserverTalker with scripted replies, RS(3,2), B=12000 in 5000-byte
 // increments / B=20000 with pieces 1 and 3 missing and indexMap [0,2,4,1,3]), checked with
@@ -426,6 +431,167 @@ static void TestRSEncodeStopsAtFailingWrite(T* t, bool pipeline) {
     }
 }
 
+// ---------------------------------------------------------------- PackTracts (store_test.go:647-746)
+
+static const core::RSChunkID packCid{0x80000555u, 5555};
+
+static std::vector<core::TSAddr> packAddrs() {
+    return {core::TSAddr{1, "a1"}, core::TSAddr{2, "a2"}, core::TSAddr{3, "a3"}};
+}
+
+static core::PackTractSpec spec(core::TractID id, std::vector<core::TSAddr> from, int version, int off, int len) {
+    core::PackTractSpec s;
+    s.ID = id;
+    s.From = std::move(from);
+    s.Version = version;
+    s.Offset = off;
+    s.Length = len;
+    return s;
+}
+
+static void TestPackTractsInvalid(T* t) {
+    memTractserverTalker tt;
+    tractserver::Store s(&tt, tractserver::Config{});
+    auto addrs = packAddrs();
+    const core::TractID tid = core::TractIDFromParts(core::BlobIDFromParts(1, 1), 0);
+    auto check = [&](int length, const std::vector<core::PackTractSpec>& srcs, const char* what) {
+        if (s.PackTracts(length, srcs, packCid) != Error::ErrInvalidArgument)
+            t->Errorf("PackTracts should have returned an error for %s", what);
+    };
+    check(-100, {}, "negative length");
+    check(1000, {spec(core::TractID{}, addrs, 1, 0, 500)}, "invalid tract id");
+    check(1000, {spec(tid, {}, 1, 0, 500)}, "no from");
+    check(1000, {spec(tid, addrs, 1, 0, 1500)}, "too long");
+    check(1000, {spec(tid, addrs, 1, 1500, 500)}, "starting too high");
+    check(1000, {spec(tid, addrs, 1, 700, 200), spec(tid, addrs, 1, 100, 200)}, "out of order");
+    if (s.PackTracts(1000, {}, core::RSChunkID{5, 5}) != Error::ErrInvalidArgument) t->Errorf("bad dest accepted");
+}
+
+static void TestPackTractsRPCError(T* t) {
+    memTractserverTalker tt;
+    tractserver::Store s(&tt, tractserver::Config{});
+    auto addrs = packAddrs();
+    const core::TractID tid1 = core::TractIDFromParts(core::BlobIDFromParts(1, 2), 0);
+    const core::TractID tid2 = core::TractIDFromParts(core::BlobIDFromParts(1, 7), 0);
+    // no read replies, should fail
+    Error err = s.PackTracts(1000, {spec(tid1, addrs, 1, 100, 200), spec(tid2, addrs, 1, 700, 200)}, packCid);
+    if (err != Error::ErrRPC) Fatalf("error from PackTracts: %s", core::String(err));
+    auto [b, rerr] = s.Read(packCid.ToTractID(), core::RSChunkVersion, 1000, 0);
+    if (rerr != Error::ErrNoSuchTract) t->Errorf("a failed pack must leave no tract (%s)", core::String(rerr));
+}
+
+static Bytes str(const char* p, size_t n) { return Bytes::copy_of(reinterpret_cast<const uint8_t*>(p), n); }
+
+static void TestPackTracts(T* t) {
+    memTractserverTalker tt;
+    tractserver::Store s(&tt, tractserver::Config{});
+    auto addrs = packAddrs();
+    const core::TractID tid1 = core::TractIDFromParts(core::BlobIDFromParts(1, 2), 0);
+    const core::TractID tid2 = core::TractIDFromParts(core::BlobIDFromParts(1, 7), 0);
+    const std::string data1 = "this is some data", data2 = "this is some more data";
+    // tract 1: first one fails, should fall back to second
+    tt.addCtlReadReply(addrs[0].Host, str("oops", 4), Error::ErrRPC);
+    tt.addCtlReadReply(addrs[1].Host, str(data1.data(), data1.size()), Error::ErrEOF);
+    // tract 2: first one has wrong length, second is corrupt, third is ok
+    tt.addCtlReadReply(addrs[0].Host, str("wrong length", 12), Error::ErrEOF);
+    tt.addCtlReadReply(addrs[1].Host, Bytes(), Error::ErrCorruptData);
+    tt.addCtlReadReply(addrs[2].Host, str(data2.data(), data2.size()), Error::ErrEOF);
+    const int n1 = static_cast<int>(data1.size()), n2 = static_cast<int>(data2.size());
+    Error err = s.PackTracts(n1 + n2 + 10, {spec(tid1, addrs, 1, 2, n1), spec(tid2, addrs, 1, n1 + 5, n2)}, packCid);
+    if (err != Error::NoError) Fatalf("error from PackTracts: %s", core::String(err));
+    // read it back
+    auto [b, rerr] = s.Read(packCid.ToTractID(), core::RSChunkVersion, 1000, 0);
+    if (rerr != Error::ErrEOF) Fatalf("error reading back packed tract: %s", core::String(rerr));
+    static const char want[] = "\x00\x00this is some data\x00\x00\x00this is some more data\x00\x00\x00\x00\x00";
+    const size_t wn = sizeof(want) - 1;
+    if (b.len() != wn || std::memcmp(b.data(), want, wn) != 0) t->Errorf("wrong data (len %zu, want %zu)", b.len(), wn);
+}
+
+// Routes CtlReads to the data tractservers' Stores (their packed pieces) or to a source
+// host holding whole tracts; records CtlWrites (the parity windows).
+class ClusterTalker : public tractserver::TractserverTalker {
+ public:
+    std::map<std::string, tractserver::Store*> stores;
+    std::map<std::string, std::map<core::TractID, Bytes>> tracts;
+    std::mutex mu;
+    std::map<std::string, std::vector<WriteReq>> writes;
+    std::pair<Bytes, Error> CtlRead(const std::string& addr, core::TractID id, int version, int length,
+                                    int64_t off) override {
+        if (auto it = stores.find(addr); it != stores.end()) return it->second->Read(id, version, length, off);
+        std::lock_guard<std::mutex> g(mu);
+        auto& host = tracts[addr];
+        auto it = host.find(id);
+        if (it == host.end()) return {Bytes(), Error::ErrNoSuchTract};
+        const Bytes& b = it->second;  // CtlRead of TractLength at 0: the whole tract, ErrEOF
+        return {Bytes::copy_of(b.data(), b.len()), static_cast<int64_t>(b.len()) < length ? Error::ErrEOF : Error::NoError};
+    }
+    Error CtlWrite(const std::string& addr, core::TractID id, int v, int64_t off, const Bytes& b) override {
+        std::lock_guard<std::mutex> g(mu);
+        writes[addr].push_back({id, v, Bytes::copy_of(b.data(), b.len()), off});
+        return Error::NoError;
+    }
+};
+
+static void TestPackThenRSEncode(T* t) {
+    const int N = 3, M = 2;
+    const int pad = 65532;             // padToLength (internal/curator/pack_tracts.go)
+    const int length = 3 * pad + 4000;
+    ClusterTalker ct;
+    std::vector<std::unique_ptr<tractserver::Store>> data;
+    for (int i = 0; i < N; ++i) {
+        data.emplace_back(new tractserver::Store(&ct, tractserver::Config{}));
+        ct.stores["d" + std::to_string(i)] = data.back().get();
+    }
+    std::mt19937_64 rng(4242);
+    std::vector<Bytes> want(N);
+    for (int i = 0; i < N; ++i) {
+        // tracts at padToLength multiples; piece i gets i + 1 tracts, the last piece a hole
+        want[i] = Bytes::make(length);
+        std::vector<core::PackTractSpec> specs;
+        for (int j = 0; j <= i; ++j) {
+            if (i == 2 && j == 1) continue;  // hole
+            const int len = 1 + static_cast<int>(rng() % (j == 3 ? 4000 : pad));
+            const core::TractID id = core::TractIDFromParts(core::BlobIDFromParts(7, 100 + 10 * i + j), 0);
+            Bytes b = randBytes(rng, len);
+            ct.tracts["src"][id] = b;
+            std::memcpy(want[i].data() + j * pad, b.data(), len);
+            specs.push_back(spec(id, {core::TSAddr{9, "gone"}, core::TSAddr{10, "src"}}, 1, j * pad, len));
+        }
+        Error err = data[i]->PackTracts(length, specs, cid.Add(i));
+        if (err != Error::NoError) Fatalf("PackTracts piece %d: %s", i, core::String(err));
+        auto [b, rerr] = data[i]->Read(cid.Add(i).ToTractID(), core::RSChunkVersion, length, 0);
+        if (rerr != Error::NoError || b.len() != static_cast<size_t>(length) ||
+            std::memcmp(b.data(), want[i].data(), length) != 0)
+            Fatalf("piece %d does not hold its tracts at their offsets", i);
+    }
+    // encEncode: the parity tractserver reads the packed pieces in increments and writes
+    // the parity to the M destinations.
+    tractserver::Store enc_ts(&ct, tractserver::Config{65536, true});
+    std::vector<core::TSAddr> srcs, dests;
+    for (int i = 0; i < N; ++i) srcs.push_back(core::TSAddr{static_cast<uint64_t>(i + 1), "d" + std::to_string(i)});
+    for (int j = 0; j < M; ++j) dests.push_back(core::TSAddr{static_cast<uint64_t>(N + j + 1), "p" + std::to_string(j)});
+    Error err = enc_ts.RSEncode(cid, length, srcs, dests, {});
+    if (err != Error::NoError) Fatalf("RSEncode: %s", core::String(err));
+    reedsolomon::Shards shards(want.begin(), want.end());
+    for (int j = 0; j < M; ++j) {
+        Bytes par = Bytes::make(length);
+        size_t got = 0;
+        for (const auto& w : ct.writes["p" + std::to_string(j)]) {
+            if (!(w.ID == cid.Add(N + j).ToTractID())) t->Errorf("parity %d written to the wrong tract", j);
+            std::memcpy(par.data() + w.Off, w.B.data(), w.B.len());
+            got += w.B.len();
+        }
+        if (got != static_cast<size_t>(length)) Fatalf("parity %d: %zu of %d bytes written", j, got, length);
+        shards.push_back(par);
+    }
+    auto [enc, e] = reedsolomon::New(N, M);
+    auto [ok, verr] = enc->Verify(shards);
+    if (verr != reedsolomon::Err::None || !ok) Fatalf("packed stripe does not verify");
+    shards[N].data()[12345] ^= 1;
+    auto [ok2, verr2] = enc->Verify(shards);
+    if (verr2 != reedsolomon::Err::None || ok2) t->Errorf("corrupted parity verified");
+}
+
 int main(int argc, char** argv) {
     const bool cpu_only = argc > 1 && std::string(argv[1]) == "--cpu";
     struct Test { const char* name; void (*fn)(T*); bool gpu; };
@@ -433,6 +599,10 @@ int main(int argc, char** argv) {
         {"TestNewErrors", TestNewErrors, false},
         {"TestShardChecks", TestShardChecks, false},
         {"TestRSEncodeArgErrors", TestRSEncodeArgErrors, false},
+        {"TestPackTractsInvalid", TestPackTractsInvalid, false},
+        {"TestPackTractsRPCError", TestPackTractsRPCError, false},
+        {"TestPackTracts", TestPackTracts, false},
+        {"TestPackThenRSEncode", TestPackThenRSEncode, true},
         {"TestRSEncode", [](T* t) { TestRSEncode(t, false); }, true},
         {"TestRSEncode/pipelined", [](T* t) { TestRSEncode(t, true); }, true},
         {"TestRSReconstruct", [](T* t) { TestRSReconstruct(t, false); }, true},

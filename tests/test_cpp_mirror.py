@@ -27,7 +27,9 @@ def _run(binary, *args):
 
 def test_cpp_mirror_cpu():
     out = _run(_build("_build/rs_test"), "--cpu")
-    assert "PASS (3 tests" in out
+    assert "PASS (6 tests, 0 failed)" in out
+    for name in ("TestPackTractsInvalid", "TestPackTractsRPCError", "TestPackTracts"):
+        assert f"--- PASS: {name}\n" in out, name
 
 
 def test_cpp_mirror_cpu_asan():
@@ -43,5 +45,5 @@ def test_cpp_mirror_cpu_asan():
 def test_cpp_mirror_gpu():
     out = _run(_build("_build/rs_test"))
     for name in ("TestRSEncode", "TestRSEncode/pipelined", "TestRSReconstruct", "TestRSReconstruct/pipelined",
-                 "TestReconstructDataIntoCallerBuffer", "TestClientRecovery"):
+                 "TestReconstructDataIntoCallerBuffer", "TestClientRecovery", "TestPackThenRSEncode"):
         assert f"--- PASS: {name}\n" in out, name
