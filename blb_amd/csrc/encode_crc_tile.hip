@@ -454,24 +454,76 @@ __device__ uint32_t shift_n(const CrcConsts* c, uint32_t r, uint64_t n) {
     return r;
 }
 
-// One thread per (row j, stripe b, block): Horner over the block's tiles (T = 2^log2t).
-__global__ __launch_bounds__(256) void tile_combine_kernel(TArgs a, uint32_t log2t, uint64_t total, uint32_t* out) {
+// Block `blk` of row-stripe jb in shard coordinates: [bs, be) (file-aligned, phase).
+__device__ __forceinline__ void block_range(const TArgs& a, uint32_t blk, uint64_t* bs, uint64_t* be) {
+    const uint64_t vs = static_cast<uint64_t>(blk) * a.block;  // file-aligned block [vs, vs + block)
+    *bs = vs > a.phase ? vs - a.phase : 0;
+    *be = vs + a.block - a.phase < a.S ? vs + a.block - a.phase : a.S;
+}
+
+// Horner over tiles [f, l] of the block [bs, be): the raw CRC of the block's bytes in them,
+// as if ending at tile l's end.
+__device__ __forceinline__ uint32_t fold_tiles(const TArgs& a, uint64_t jb, uint64_t bs, uint64_t be, uint32_t log2t,
+                                               uint64_t f, uint64_t l) {
+    const uint32_t* raw = a.raw + jb * a.tps;
+    const uint32_t* hi = a.hi + jb * a.tps;
+    const cu32 st = as_const(&a.c->pow2[log2t][0]);
+    uint32_t acc = 0u;
+    for (uint64_t i = f; i <= l; ++i) {
+        uint32_t piece = (i << log2t) < bs ? hi[i] : raw[i];  // block starts inside tile i
+        if (((i + 1) << log2t) > be && be < a.S) piece ^= hi[i];  // next block starts inside tile i
+        acc = (i == f ? 0u : apply(st, acc)) ^ piece;
+    }
+    return acc;
+}
+
+// Whole-shard frames span 512-2048 tiles: folding them in one thread per (row, stripe)
+// serialises ~1-2k matrix applies on a few thousand threads.  Blocks of more than
+// kChunk tiles fold in two levels: this kernel, one thread per (row, stripe, block, chunk of
+// kChunk tiles), then tile_combine_kernel over the chunks.
+constexpr uint32_t kChunkLog2 = 5;
+constexpr uint32_t kChunk = 1u << kChunkLog2;
+
+__global__ __launch_bounds__(256) void tile_chunk_kernel(TArgs a, uint32_t log2t, uint32_t nchunk, uint64_t total,
+                                                         uint32_t* part) {
+    const uint64_t id = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    if (id >= total) return;
+    const uint32_t c = static_cast<uint32_t>(id % nchunk);
+    const uint64_t rest = id / nchunk;
+    const uint32_t blk = static_cast<uint32_t>(rest % a.nblocks);
+    const uint64_t jb = rest / a.nblocks;
+    uint64_t bs, be;
+    block_range(a, blk, &bs, &be);
+    const uint64_t i0 = bs >> log2t, i1 = (be - 1) >> log2t;
+    const uint64_t f = i0 + (static_cast<uint64_t>(c) << kChunkLog2);
+    part[id] = f > i1 ? 0u : fold_tiles(a, jb, bs, be, log2t, f, f + kChunk - 1 < i1 ? f + kChunk - 1 : i1);
+}
+
+// One thread per (row j, stripe b, block): Horner over the block's tiles (T = 2^log2t), or
+// over its chunk partials when `part` is set.
+__global__ __launch_bounds__(256) void tile_combine_kernel(TArgs a, uint32_t log2t, uint64_t total, uint32_t* out,
+                                                           uint32_t nchunk, const uint32_t* part) {
     const uint64_t id = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
     if (id >= total) return;
     const uint32_t blk = static_cast<uint32_t>(id % a.nblocks);
     const uint64_t jb = id / a.nblocks;  // j * B + b
-    const uint64_t vs = static_cast<uint64_t>(blk) * a.block;  // file-aligned block [vs, vs + block)
-    const uint64_t bs = vs > a.phase ? vs - a.phase : 0;
-    const uint64_t be = vs + a.block - a.phase < a.S ? vs + a.block - a.phase : a.S;
-    const uint32_t* raw = a.raw + jb * a.tps;
-    const uint32_t* hi = a.hi + jb * a.tps;
-    const cu32 st = as_const(&a.c->pow2[log2t][0]);
+    uint64_t bs, be;
+    block_range(a, blk, &bs, &be);
     const uint64_t i0 = bs >> log2t, i1 = (be - 1) >> log2t;
-    uint32_t acc = 0u;
-    for (uint64_t i = i0; i <= i1; ++i) {
-        uint32_t piece = (i << log2t) < bs ? hi[i] : raw[i];  // block starts inside tile i
-        if (((i + 1) << log2t) > be && be < a.S) piece ^= hi[i];  // next block starts inside tile i
-        acc = (i == i0 ? 0u : apply(st, acc)) ^ piece;
+    uint32_t acc;
+    if (part) {
+        const cu32 sc = as_const(&a.c->pow2[log2t + kChunkLog2][0]);  // S_{kChunk * T}
+        const uint32_t* p = part + id * nchunk;
+        acc = 0u;
+        for (uint32_t c = 0; c < nchunk; ++c) {
+            const uint64_t f = i0 + (static_cast<uint64_t>(c) << kChunkLog2);
+            if (f > i1) break;
+            const uint64_t n = i1 - f + 1 < kChunk ? i1 - f + 1 : kChunk;  // tiles in chunk c
+            if (c > 0) acc = n == kChunk ? apply(sc, acc) : shift_n(a.c, acc, n << log2t);
+            acc ^= p[c];
+        }
+    } else {
+        acc = fold_tiles(a, jb, bs, be, log2t, i0, i1);
     }
     const uint64_t tail = ((i1 + 1) << log2t) - be;
     if (tail) acc = shift_n(a.c, acc, kOrd - tail);
@@ -639,13 +691,29 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
         hipLaunchKernelGGL(pick(in.k, in.rows, true), dim3(in.B), dim3(kTThreads), 0, stream, a);
         e = hipGetLastError();
     }
+    const uint64_t total = static_cast<uint64_t>(in.rows) * in.B * a.nblocks;
+    // Tiles a block can touch: ceil(block / T) + 1 (an unaligned block straddles one more).
+    const uint64_t max_tiles = ((a.block + (uint64_t{1} << log2t) - 1) >> log2t) + 1;
+    const uint32_t nchunk = max_tiles > 2 * kChunk ? static_cast<uint32_t>((max_tiles + kChunk - 1) >> kChunkLog2) : 0u;
+    uint32_t* part = nullptr;
+    if (e == hipSuccess && nchunk) {
+        e = hipMallocAsync(reinterpret_cast<void**>(&part), total * nchunk * sizeof(uint32_t), stream);
+        if (e == hipSuccess) {
+            const uint64_t nthreads = total * nchunk;
+            hipLaunchKernelGGL(tile_chunk_kernel, dim3(static_cast<unsigned>((nthreads + 255) / 256)), dim3(256), 0,
+                               stream, a, log2t, nchunk, nthreads, part);
+            e = hipGetLastError();
+        }
+    }
     if (e == hipSuccess) {
-        const uint64_t total = static_cast<uint64_t>(in.rows) * in.B * a.nblocks;
         hipLaunchKernelGGL(tile_combine_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
-                           stream, a, log2t, total, in.crc);
+                           stream, a, log2t, total, in.crc, nchunk, part);
         e = hipGetLastError();
     }
-    const hipError_t f = hipFreeAsync(buf, stream);
+    hipError_t f = hipSuccess;
+    if (part) f = hipFreeAsync(part, stream);
+    const hipError_t g = hipFreeAsync(buf, stream);
+    if (f == hipSuccess) f = g;
     return e != hipSuccess ? e : f;
 }
 

@@ -184,7 +184,10 @@ def test_encode_crc_phase_and_seed_shapes(oracle_lib, k, m):
     rng = np.random.default_rng(k * 100 + m)
     enc = rs.New(k, m)
     cases = [(4128704, 65532, 256), (1 << 20, 65532, 65528), (200000, 4096, 4092), (8192 * 3 + 48, 8192, 4),
-             (70001, 65532, 1000), (65536, 65532, 65531), (4096, 65532, 65000), (16, 65532, 0), (1 << 20, 0, 0)]
+             (70001, 65532, 1000), (65536, 65532, 65531), (4096, 65532, 65000), (16, 65532, 0), (1 << 20, 0, 0),
+             # blocks of > 64 tiles: the two-level tile fold (chunks of 32 tiles), with block
+             # ends inside tiles, a partial last tile and a straddling first block
+             ((3 << 20) + 16, 4 << 20, 12), (6 << 20, (2 << 20) + 4, 1000), ((2 << 20) + 48, 1 << 20, 0)]
     for S, block, phase in cases:
         B = 2
         host = rng.integers(0, 256, (B, k + m, S), dtype=np.uint8)
