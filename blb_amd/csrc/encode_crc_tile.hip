@@ -177,6 +177,11 @@ __device__ __forceinline__ void lane_shift(const uint32_t* lmat, uint32_t lane, 
 #define BLBRS_ECT_NIB 1
 #endif
 constexpr bool kNib = BLBRS_ECT_NIB != 0;
+#ifndef BLBRS_ECT_SPREAD
+#define BLBRS_ECT_SPREAD 1
+#endif
+// Row totals through the nibble factors with the A factor spread one row per lane (needs kNib).
+constexpr bool kSpread = kNib && BLBRS_ECT_SPREAD != 0;
 
 __device__ __forceinline__ uint32_t apply_nib(const uint32_t* t, uint32_t c) {
     uint32_t v[8];
@@ -232,12 +237,15 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
     // bytes past it (hi).  One code path for both keeps the register footprint of the rare
     // split wave at that of the others.
     uint32_t o_raw[MR], o_hi[MR];
+    uint32_t r_raw = 0u, r_hi = 0u;  // kSpread: this lane's row (lane & 7) of the wave totals
     const uint32_t passes = split && wave == o_wave ? 2u : 1u;
 #pragma unroll 1
     for (uint32_t pass = 0; pass < passes; ++pass) {
         uint32_t crc[MR];
 #pragma unroll
         for (int j = 0; j < MR; ++j) crc[j] = 0u;
+        // One masked code path for both passes: separate unmasked pass-0 chains let the
+        // compiler hoist every lookup (165 instead of 112 VGPRs at RS(6,3)).
         if constexpr (kSlice == 8 && !(kFlags & 2)) {
 #pragma unroll
             for (int d = 0; d < NV; d += 2) {
@@ -261,6 +269,32 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
         }
         // Shift each lane's chain to its row end (S_{LC*(63-lane)} from LDS) and XOR over the
         // wave; the row -> tile-end shift is applied once per row in the final reduction.
+        if constexpr (kSpread && !(kFlags & 4)) {
+            // S_{LC*e} = A_{e>>3} B_{e&7} (e = 63 - lane): B on every row, XOR over the lane's
+            // 8-lane group (whose values then agree), lane h = lane & 7 takes row h for A (one
+            // apply instead of MR), XOR over the 8 groups.  Lane h ends with row h's total.
+            const uint32_t e = 63u - lane;
+            const uint32_t* tb = lmat + (e & 7u) * kNibStride;
+            const uint32_t* ta = lmat + (8u + (e >> 3)) * kNibStride;
+            uint32_t row = 0u;
+#pragma unroll
+            for (int j = 0; j < MR; ++j) {
+                uint32_t t = apply_nib(tb, crc[j]);
+                t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0xB1, 0xF, 0xF, false));
+                t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0x4E, 0xF, 0xF, false));
+                t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0x141, 0xF, 0xF, false));
+                row = (lane & 7u) == static_cast<uint32_t>(j) ? t : row;
+            }
+            row = apply_nib(ta, row);
+            row ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(row), 0x128, 0xF, 0xF, false));  // row_ror:8
+            auto r16 = __builtin_amdgcn_permlane16_swap(row, row, false, false);
+            row = r16[0] ^ r16[1];
+            auto r32 = __builtin_amdgcn_permlane32_swap(row, row, false, false);
+            row = r32[0] ^ r32[1];
+            if (pass == 0) r_raw = row;
+            else r_hi = row;
+            continue;
+        }
         uint32_t v[MR];
         if constexpr (kFlags & 4) {
 #pragma unroll
@@ -277,15 +311,23 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
             else o_hi[jj] = v[jj];
         }
     }
-    if (passes == 1)
-#pragma unroll
-        for (int jj = 0; jj < MR; ++jj) o_hi[jj] = split && wave > o_wave ? o_raw[jj] : 0u;
-    if (lane == 0)
-#pragma unroll
-        for (int j = 0; j < MR; ++j) {
-            red[0][wave][j] = o_raw[j];
-            red[1][wave][j] = o_hi[j];
+    if constexpr (kSpread && !(kFlags & 4)) {
+        if (passes == 1) r_hi = split && wave > o_wave ? r_raw : 0u;
+        if (lane < static_cast<uint32_t>(MR)) {
+            red[0][wave][lane] = r_raw;
+            red[1][wave][lane] = r_hi;
         }
+    } else {
+        if (passes == 1)
+#pragma unroll
+            for (int jj = 0; jj < MR; ++jj) o_hi[jj] = split && wave > o_wave ? o_raw[jj] : 0u;
+        if (lane == 0)
+#pragma unroll
+            for (int j = 0; j < MR; ++j) {
+                red[0][wave][j] = o_raw[j];
+                red[1][wave][j] = o_hi[j];
+            }
+    }
     __syncthreads();
     // Row ends -> tile end, spread over lanes: wave 0 folds the raw values, wave 1 the hi
     // values; lane 8j + s takes half s&1 of S_{64*LC*(3-w)} (w = s>>1, 16 columns) on row j's
