@@ -177,6 +177,10 @@ __device__ __forceinline__ void lane_shift(const uint32_t* lmat, uint32_t lane, 
 #define BLBRS_ECT_NIB 1
 #endif
 constexpr bool kNib = BLBRS_ECT_NIB != 0;
+#ifndef BLBRS_ECT_TABSEQ
+#define BLBRS_ECT_TABSEQ 0
+#endif
+constexpr int kTabSeq = BLBRS_ECT_TABSEQ;  // coefficient-load distance in pairs (0 = unconstrained)
 #ifndef BLBRS_ECT_SPREAD
 #define BLBRS_ECT_SPREAD 1
 #endif
@@ -459,9 +463,16 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
             cu32 tables = as_const(a.tables);
             asm volatile("" : "+s"(tables));
 #pragma unroll
-            for (int c = 0; c + 1 < K; c += 2)
+            for (int c = 0; c + 1 < K; c += 2) {
+                if constexpr (kTabSeq > 0) {
+                    // The pair's coefficient loads wait for the accumulators of kTabSeq pairs
+                    // back: without it all K*MR*5 table words are loaded up front and spill
+                    // SGPRs (RS(12,5): 300 words).
+                    if (c >= 2 * kTabSeq) asm volatile("" : "+s"(tables) : "v"(acc[0][0]));
+                }
                 madd2<MR, NV>(Groups<NV>(x[c]), [&](int r) { return tables + (r * K + c) * 5; }, Groups<NV>(x[c + 1]),
                               [&](int r) { return tables + (r * K + c + 1) * 5; }, acc, MR);
+            }
             if constexpr (K & 1)
                 madd<MR, NV>(Groups<NV>(x[K - 1]), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, MR);
         }

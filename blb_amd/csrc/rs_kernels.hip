@@ -251,11 +251,21 @@ constexpr int kMaxTemplRows = 5;
 //  * store mode: U = 4 chunks per lane (16 KiB tiles) when K + MR <= 9, else U = 2 -- wider
 //    shapes at U = 4 drop to one wave per SIMD (RS(10,4) 4.6 vs 6.2 TB/s);
 //  * verify mode (check shards prefetched with the inputs): U = 2 -- 6.8 TB/s, faster than
-//    a plain 9-shard read stream; U = 4 needs too many VGPRs;
+//    a plain 9-shard read stream; U = 4 needs too many VGPRs; U = 1 when K + MR > 13:
+//    RS(12,5) at U = 2 holds 256 VGPRs (one wave per SIMD) and verified in 20.0 ms, at U = 1
+//    147 VGPRs and 13.4 ms; RS(10,4) 10.45 -> 9.9-10.3 ms (tools/code_ab.py, r02);
 //  * one tile per block in dispatch order (no persistent grid-stride), with each XCD given
 //    a contiguous eighth of the tiles: +10-16 % over a resident persistent grid.
 constexpr int kNT = 3;
-constexpr int pick_u(int K, int MR, int MODE) { return (MODE == 0 && K > 0 && K + MR <= 9) ? 4 : 2; }
+#ifndef BLBRS_U_WIDE
+#define BLBRS_U_WIDE 2         // store mode, K + MR > 9
+#endif
+#ifndef BLBRS_U_VERIFY_WIDE
+#define BLBRS_U_VERIFY_WIDE 1  // verify mode, K + MR > 13
+#endif
+constexpr int pick_u(int K, int MR, int MODE) {
+    return MODE == 0 ? ((K > 0 && K + MR <= 9) ? 4 : BLBRS_U_WIDE) : (K + MR > 13 ? BLBRS_U_VERIFY_WIDE : 2);
+}
 
 template <int K, int MR, int MODE, int ADDR>
 constexpr KernelFn fn_of() { return rs_code_kernel<K, MR, MODE, ADDR, pick_u(K, MR, MODE), kNT>; }
