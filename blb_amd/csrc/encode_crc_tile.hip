@@ -177,10 +177,12 @@ __device__ __forceinline__ void lane_shift(const uint32_t* lmat, uint32_t lane, 
 #define BLBRS_ECT_NIB 1
 #endif
 constexpr bool kNib = BLBRS_ECT_NIB != 0;
+// Coefficient loads one input pair behind the accumulators (0 = unconstrained): no SGPR
+// spills at RS(12,5) / RS(10,4), 15.82 vs 16.18 ms and 11.12 vs 11.22 ms (profiles/r02/ect_ab/r2r_tabseq).
 #ifndef BLBRS_ECT_TABSEQ
-#define BLBRS_ECT_TABSEQ 0
+#define BLBRS_ECT_TABSEQ 1
 #endif
-constexpr int kTabSeq = BLBRS_ECT_TABSEQ;  // coefficient-load distance in pairs (0 = unconstrained)
+constexpr int kTabSeq = BLBRS_ECT_TABSEQ;
 #ifndef BLBRS_ECT_SPREAD
 #define BLBRS_ECT_SPREAD 1
 #endif
