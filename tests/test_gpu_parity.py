@@ -225,8 +225,9 @@ def test_too_many_erasures_and_all_present():
     assert all(np.array_equal(a, b) for a, b in zip(sh, before))
 
 
-def test_verify_detects_corruption(dev):
-    k, m, S, B = 6, 3, 65536 + 7, 5
+@pytest.mark.parametrize("k,m", [(6, 3), (10, 4), (12, 5)])  # (10,4), (12,5): verify at U = 1
+def test_verify_detects_corruption(dev, k, m):
+    S, B = 65536 + 7, 5
     enc = rs.New(k, m)
     st = torch.randint(0, 256, (B, k + m, S), dtype=torch.uint8, device=dev)
     enc.EncodeBatch(st)
