@@ -44,42 +44,43 @@ using namespace dev;
 
 constexpr int kTThreads = 256;                     // 4 waves, one row each
 constexpr uint64_t kOrd = 0x7FFFFFFFull;            // S_{kOrd} = I (checked on the host)
-#ifndef BLBRS_ECT_COPIES
-#define BLBRS_ECT_COPIES 1
-#endif
-constexpr int kCopies = BLBRS_ECT_COPIES;           // interleaved copies of the slicing tables
-// Tuning builds only (tools/ect_variants.sh): 1 = skip the constant staging, 2 = skip the
-// slicing chains, 4 = skip the lane shifts.  Results are wrong with any bit set.
+// Tuning builds only (tools/ect_variants.sh; the cost split in profiles/r02/ect_ab): 1 = skip
+// the constant staging, 2 = skip the slicing chains, 4 = skip the lane shifts.  Results are
+// wrong with any bit set.
 #ifndef BLBRS_ECT_FLAGS
 #define BLBRS_ECT_FLAGS 0
 #endif
 constexpr int kFlags = BLBRS_ECT_FLAGS;
 
-// Shift matrices (v = 0: LC 64, v = 1: LC 32): lanemat[v][i][l] = column i of S_{LC*(63-l)}
-// (lane chunk end -> end of the wave's row; staged in LDS per workgroup, one conflict-free
-// column read per lane) and wavemat[v][w] = S_{64*LC*(3-w)} (row end -> tile end).
-struct TileConsts {
-    uint32_t lanemat[3][32][64];
-    uint32_t wavemat[3][4][32];
-    uint32_t tab8[8][256];  // slicing-by-8 tables: tab8[k][i] = CRC of byte i followed by k zeros
-    // Nibble tables of the lane shifts, two factors: S_{LC*(63-l)} = A_{(63-l)>>3} B_{(63-l)&7}
-    // with B_b = S_{LC*b} (tables 0..7) and A_a = S_{8*LC*a} (tables 8..15); table t, nibble
-    // k, value v at [t * kNibStride + 16 * k + v] = the matrix applied to v << 4k.
-    uint32_t nib[3][16 * 136];
-};
-constexpr uint32_t kNibStride = 136;  // 128 + 8 words: the 16 tables start on 8 different banks
+// Lane chunks: LC = 32 bytes (8 KiB tiles) for every shape but the widest, 16 bytes (4 KiB
+// tiles) when k + rows >= 17: half the input registers (RS(12,5) at 32-byte chunks needs 256
+// VGPRs, 25.4 vs 16.8 ms at the time), twice the lane shifts per byte.  RS(10,4) is faster at
+// 32 (11.4 vs 12.7 ms).  64-byte chunks (16 KiB tiles, 2 waves per SIMD) were slower.
+constexpr int lc_for(int k, int rows) { return k + rows >= 17 ? 16 : 32; }
+constexpr int lc_index(int lc) { return lc == 32 ? 0 : 1; }
 
-// Slicing-by-8 halves the chain's dependent LDS round trips (4 steps per 32-byte lane chunk
-// instead of 8; the second dword's lookups do not wait for the chain): RS(6,3) B=1024
-// 13.5-13.75 ms vs 13.7-13.95 ms for slicing-by-4 (tools/ect_ab.py, interleaved builds).
-#ifndef BLBRS_ECT_SLICE
-#define BLBRS_ECT_SLICE 8
+// Per LC: the nibble tables of the lane shifts and the row-end -> tile-end matrices.
+//   nib: S_{LC*e} (e = 63 - lane: lane chunk end -> end of the wave's row) in two factors,
+//        S_{LC*e} = A_{e>>3} B_{e&7} with B_b = S_{LC*b} (tables 0..7) and A_a = S_{8*LC*a}
+//        (tables 8..15); table t, nibble k, value v at [t * kNibStride + 16 * k + v] is the
+//        matrix applied to v << 4k.  16 lookups per value instead of 32 columns x 2 VALU.
+//   wavemat[w] = S_{64*LC*(3-w)} (row end -> tile end), column-major.
+// tab8[k][i] = CRC of byte i followed by k zero bytes (slicing-by-8).
+constexpr uint32_t kNibStride = 136;  // 128 + 8 words: the 16 tables start on 8 different banks
+constexpr uint32_t kNibWords = 16 * kNibStride;
+struct TileConsts {
+    uint32_t nib[2][kNibWords];
+    uint32_t wavemat[2][4][32];
+    uint32_t tab8[8][256];
+};
+
+// Coefficient loads one input pair behind the accumulators (0 = unconstrained): without it
+// all K*MR*5 table words are loaded up front and spill SGPRs (RS(12,5): 300 words, 70
+// spills); with it RS(12,5) 15.82 vs 16.18 ms, RS(10,4) 11.12 vs 11.22 (r2r_tabseq).
+#ifndef BLBRS_ECT_TABSEQ
+#define BLBRS_ECT_TABSEQ 1
 #endif
-constexpr int kSlice = BLBRS_ECT_SLICE;  // slicing-by-4 (CrcConsts tables) or -by-8 (tab8)
-#ifndef BLBRS_ECT_PREFETCH
-#define BLBRS_ECT_PREFETCH 1
-#endif
-constexpr bool kPrefetch = BLBRS_ECT_PREFETCH != 0;
+constexpr int kTabSeq = BLBRS_ECT_TABSEQ;
 
 struct TArgs {
     const uint32_t* tables;
@@ -92,41 +93,18 @@ struct TArgs {
     uint32_t B, tps, xcd_remap, nblocks;
     uint32_t tps_full;        // whole tiles per stripe (the main grid); tps - 1 when S % T != 0
     const CrcConsts* c;
-    const uint32_t* lanemat;  // [32][64] for this LC
+    const uint32_t* nib;      // [kNibWords] for this LC
     const uint32_t* tab8;     // [8][256]
     const uint32_t* wavemat;  // [4][32] for this LC
     uint32_t* raw;            // [(j * B + b) * tps + tile]: raw CRC of the tile's bytes
     uint32_t* hi;             // same index: raw CRC of the bytes past the tile's block boundary
 };
 
-// 32-byte lane chunks for every shape: 8 KiB tiles, <= 165 VGPRs for rows <= 4 (3-4 waves per
-// SIMD); 64-byte chunks (16 KiB tiles, 2 waves per SIMD) measured slower.
-// 16-byte chunks (4 KiB tiles) for the widest shapes: half the input registers, twice the
-// lane shifts per byte.  RS(12,5) at 32-byte chunks needs 256 VGPRs (25.4 ms, B=512); at 16
-// it fits 94 (16.8 ms, the segment kernel's time, and it takes file phases).  RS(10,4) is
-// faster at 32 (11.4 vs 12.7 ms).
-#ifndef BLBRS_ECT_LC16_MIN
-#define BLBRS_ECT_LC16_MIN 17
-#endif
-constexpr int lc_for(int k, int rows) { return k + rows >= BLBRS_ECT_LC16_MIN ? 16 : 32; }
-constexpr int lc_index(int lc) { return lc == 64 ? 0 : lc == 32 ? 1 : 2; }
-
-// One slicing-by-4 step over C-copy tables (table 3-k serves byte k).
-template <int C>
-__device__ __forceinline__ uint32_t slice4c(const uint32_t* tab, uint32_t copy, uint32_t x) {
-    uint32_t v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t e = __builtin_amdgcn_ubfe(x, 8 * k, 8);
-        v[k] = tab[(3 - k) * 256 * C + e * C + copy];
-    }
-    return xor3(v[0], v[1], v[2]) ^ v[3];
-}
-
 // XOR over the 64 lanes, result in every lane, all on the VALU: DPP inside each 16-lane row
 // (swap neighbours, swap pairs, half-row mirror, row mirror), then permlane16/32 swaps across
-// rows -- no ds_bpermute through the LDS pipe the slicing lookups need.
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+// rows -- no ds_bpermute through the LDS pipe the slicing lookups need.  (Cost-split builds
+// only: the shipped path reduces through row_totals.)
+[[maybe_unused]] __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
     v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
     v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
     v ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0x141, 0xF, 0xF, false));  // half-row mirror
@@ -137,58 +115,6 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
     return r32[0] ^ r32[1];
 }
 
-// o = S_{LC*(63-lane)} c per row (and the same for the hi chains when HI): the lane matrix's
-// 32 columns are read from LDS four at a time, one group ahead of the group being applied,
-// with scheduling fences in between -- without them the compiler hoists all 32 reads and
-// holds 32 registers through the whole CRC (which then no longer fits beside the next
-// tile's inputs).
-template <int MR>
-__device__ __forceinline__ void lane_shift(const uint32_t* lmat, uint32_t lane, const uint32_t (&crc)[MR],
-                                           uint32_t (&o)[MR]) {
-#pragma unroll
-    for (int j = 0; j < MR; ++j) o[j] = 0u;
-    uint32_t cur[4], nxt[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) cur[u] = lmat[u * 64 + lane];
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-        if (g < 7) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) nxt[u] = lmat[((g + 1) * 4 + u) * 64 + lane];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = g * 4 + u;
-#pragma unroll
-            for (int j = 0; j < MR; ++j)
-                o[j] = __builtin_amdgcn_bitop3_b32(
-                    o[j], static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(crc[j]), i, 1)), cur[u], 0x78);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
-    }
-}
-
-// Lane shifts by nibble tables (default) or by 32 columns: RS(12,5) 15.99 vs 16.32 ms,
-// RS(10,4) 11.02 vs 11.11, RS(6,3) 13.11 vs 13.10 (tools/ect_ab.py, profiles/r02/ect_ab/r2n).
-#ifndef BLBRS_ECT_NIB
-#define BLBRS_ECT_NIB 1
-#endif
-constexpr bool kNib = BLBRS_ECT_NIB != 0;
-// Coefficient loads one input pair behind the accumulators (0 = unconstrained): no SGPR
-// spills at RS(12,5) / RS(10,4), 15.82 vs 16.18 ms and 11.12 vs 11.22 ms (profiles/r02/ect_ab/r2r_tabseq).
-#ifndef BLBRS_ECT_TABSEQ
-#define BLBRS_ECT_TABSEQ 1
-#endif
-constexpr int kTabSeq = BLBRS_ECT_TABSEQ;
-#ifndef BLBRS_ECT_SPREAD
-#define BLBRS_ECT_SPREAD 1
-#endif
-// Row totals through the nibble factors with the A factor spread one row per lane (needs kNib).
-constexpr bool kSpread = kNib && BLBRS_ECT_SPREAD != 0;
-
 __device__ __forceinline__ uint32_t apply_nib(const uint32_t* t, uint32_t c) {
     uint32_t v[8];
 #pragma unroll
@@ -196,20 +122,37 @@ __device__ __forceinline__ uint32_t apply_nib(const uint32_t* t, uint32_t c) {
     return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
 }
 
-// o = S_{LC*(63-lane)} c per row through two nibble-table factors (16 LDS lookups and ~40
-// VALU per value instead of 32 columns x 2 VALU).
+// The wave's row totals: row j's sum over lanes of S_{LC*(63-lane)} crc_lane[j].  B factor on
+// every row, XOR over the lane's 8-lane group (whose values then agree), lane h = lane & 7
+// takes row h for the A factor (one apply instead of MR), XOR over the 8 groups.  Lane h
+// returns row h's total (h < MR).  Per lane: MR + 1 factor applies instead of 2 MR, one
+// 8-group reduction instead of MR wave reductions (RS(12,5) 16.6 -> 15.6 ms, r2q_spread).
 template <int MR>
-__device__ __forceinline__ void lane_shift_nib(const uint32_t* nt, uint32_t lane, const uint32_t (&crc)[MR],
-                                               uint32_t (&o)[MR]) {
+__device__ __forceinline__ uint32_t row_totals(const uint32_t* nt, uint32_t lane, const uint32_t (&crc)[MR]) {
+    static_assert(MR <= 8, "one row per lane of an 8-lane group");
     const uint32_t e = 63u - lane;
     const uint32_t* tb = nt + (e & 7u) * kNibStride;
     const uint32_t* ta = nt + (8u + (e >> 3)) * kNibStride;
+    uint32_t row = 0u;
 #pragma unroll
-    for (int j = 0; j < MR; ++j) o[j] = apply_nib(ta, apply_nib(tb, crc[j]));
+    for (int j = 0; j < MR; ++j) {
+        uint32_t t = apply_nib(tb, crc[j]);
+        t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0xB1, 0xF, 0xF, false));
+        t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0x4E, 0xF, 0xF, false));
+        t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0x141, 0xF, 0xF, false));
+        row = (lane & 7u) == static_cast<uint32_t>(j) ? t : row;
+    }
+    row = apply_nib(ta, row);
+    row ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(row), 0x128, 0xF, 0xF, false));  // row_ror:8
+    auto r16 = __builtin_amdgcn_permlane16_swap(row, row, false, false);
+    row = r16[0] ^ r16[1];
+    auto r32 = __builtin_amdgcn_permlane32_swap(row, row, false, false);
+    return r32[0] ^ r32[1];
 }
 
 // One slicing-by-8 step: x = crc ^ first dword, y = second dword (byte k of x: table 7-k,
-// byte k of y: table 3-k).  The y lookups do not depend on the chain.
+// byte k of y: table 3-k).  The y lookups do not depend on the chain, and a 32-byte lane
+// chunk takes 4 dependent LDS round trips instead of 8 (slicing-by-4: +1.5 % at RS(6,3)).
 __device__ __forceinline__ uint32_t slice8(const uint32_t* tab, uint32_t x, uint32_t y) {
     uint32_t v[8];
 #pragma unroll
@@ -221,16 +164,15 @@ __device__ __forceinline__ uint32_t slice8(const uint32_t* tab, uint32_t x, uint
 }
 
 // The CRC part of one tile: this lane's LC contiguous parity bytes per row (acc, already in
-// lane_contiguous order) -> raw / hi of the tile, written by threads 0..MR-1.  `red` is the
-// workgroup's reduction buffer for this tile (2 x 4 x MR words); one __syncthreads inside.
+// lane_contiguous order) -> raw / hi of the tile, written by waves 0 and 1.  `red` is the
+// workgroup's reduction buffer (2 x 4 x MR words); one __syncthreads inside.
 template <int MR, int LC>
 __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC / 4], const uint32_t* tab,
-                                         const uint32_t* lmat, const uint32_t* wm, uint32_t (*red)[4][MR], uint64_t tile_off,
-                                         uint64_t at0, uint32_t tid, uint32_t lane, uint32_t wave) {
+                                         const uint32_t* nib, const uint32_t* wm, uint32_t (*red)[4][MR],
+                                         uint64_t tile_off, uint64_t at0, uint32_t tid, uint32_t lane, uint32_t wave) {
     constexpr int NV = LC / 4;
     constexpr uint32_t kRow = 64u * LC;
     constexpr uint32_t kTile = 4u * kRow;
-    const uint32_t copy = lane % kCopies;
     // The first block boundary after the tile start; inside the tile -> the bytes past it
     // get their own raw CRC (hi).  Only the wave whose row holds the boundary needs a masked
     // chain: in earlier waves hi = 0, in later ones hi = the full raw CRC.
@@ -240,99 +182,52 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
     const uint32_t o_wave = o / kRow;
     const uint32_t mine = LC * tid;
     // Pass 0: every byte (raw).  Pass 1, only in the wave whose row holds the boundary: the
-    // bytes past it (hi).  One code path for both keeps the register footprint of the rare
-    // split wave at that of the others.
-    uint32_t o_raw[MR], o_hi[MR];
-    uint32_t r_raw = 0u, r_hi = 0u;  // kSpread: this lane's row (lane & 7) of the wave totals
+    // bytes past it (hi).  One masked code path for both keeps the register footprint of the
+    // rare split wave at that of the others; separate unmasked pass-0 chains let the compiler
+    // hoist every lookup (165 instead of 112 VGPRs at RS(6,3)).
+    uint32_t r_raw = 0u, r_hi = 0u;  // this lane's row (lane & 7) of the wave totals
+    uint32_t f_raw[MR], f_hi[MR];    // BLBRS_ECT_FLAGS & 4 only: per-row wave XORs
     const uint32_t passes = split && wave == o_wave ? 2u : 1u;
 #pragma unroll 1
     for (uint32_t pass = 0; pass < passes; ++pass) {
         uint32_t crc[MR];
 #pragma unroll
         for (int j = 0; j < MR; ++j) crc[j] = 0u;
-        // One masked code path for both passes: separate unmasked pass-0 chains let the
-        // compiler hoist every lookup (165 instead of 112 VGPRs at RS(6,3)).
-        if constexpr (kSlice == 8 && !(kFlags & 2)) {
 #pragma unroll
-            for (int d = 0; d < NV; d += 2) {
-                const bool keep0 = pass == 0 || mine + 4u * d >= o;
-                const bool keep1 = pass == 0 || mine + 4u * d + 4u >= o;
-#pragma unroll
-                for (int j = 0; j < MR; ++j)
-                    crc[j] = slice8(tab, crc[j] ^ (keep0 ? acc[j][d] : 0u), keep1 ? acc[j][d + 1] : 0u);
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < NV; ++d) {
-                const bool keep = pass == 0 || mine + 4u * d >= o;
-#pragma unroll
-                for (int j = 0; j < MR; ++j) {
-                    const uint32_t w = keep ? acc[j][d] : 0u;
-                    if constexpr (kFlags & 2) crc[j] ^= w;
-                    else crc[j] = slice4c<kCopies>(tab, copy, crc[j] ^ w);
-                }
-            }
-        }
-        // Shift each lane's chain to its row end (S_{LC*(63-lane)} from LDS) and XOR over the
-        // wave; the row -> tile-end shift is applied once per row in the final reduction.
-        if constexpr (kSpread && !(kFlags & 4)) {
-            // S_{LC*e} = A_{e>>3} B_{e&7} (e = 63 - lane): B on every row, XOR over the lane's
-            // 8-lane group (whose values then agree), lane h = lane & 7 takes row h for A (one
-            // apply instead of MR), XOR over the 8 groups.  Lane h ends with row h's total.
-            const uint32_t e = 63u - lane;
-            const uint32_t* tb = lmat + (e & 7u) * kNibStride;
-            const uint32_t* ta = lmat + (8u + (e >> 3)) * kNibStride;
-            uint32_t row = 0u;
+        for (int d = 0; d < NV; d += 2) {
+            const bool keep0 = pass == 0 || mine + 4u * d >= o;
+            const bool keep1 = pass == 0 || mine + 4u * d + 4u >= o;
 #pragma unroll
             for (int j = 0; j < MR; ++j) {
-                uint32_t t = apply_nib(tb, crc[j]);
-                t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0xB1, 0xF, 0xF, false));
-                t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0x4E, 0xF, 0xF, false));
-                t ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(t), 0x141, 0xF, 0xF, false));
-                row = (lane & 7u) == static_cast<uint32_t>(j) ? t : row;
+                const uint32_t x = crc[j] ^ (keep0 ? acc[j][d] : 0u), y = keep1 ? acc[j][d + 1] : 0u;
+                crc[j] = (kFlags & 2) ? x ^ y : slice8(tab, x, y);
             }
-            row = apply_nib(ta, row);
-            row ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(row), 0x128, 0xF, 0xF, false));  // row_ror:8
-            auto r16 = __builtin_amdgcn_permlane16_swap(row, row, false, false);
-            row = r16[0] ^ r16[1];
-            auto r32 = __builtin_amdgcn_permlane32_swap(row, row, false, false);
-            row = r32[0] ^ r32[1];
-            if (pass == 0) r_raw = row;
-            else r_hi = row;
-            continue;
         }
-        uint32_t v[MR];
         if constexpr (kFlags & 4) {
 #pragma unroll
-            for (int jj = 0; jj < MR; ++jj) v[jj] = crc[jj];
-        } else if constexpr (kNib) {
-            lane_shift_nib<MR>(lmat, lane, crc, v);
+            for (int j = 0; j < MR; ++j) (pass == 0 ? f_raw : f_hi)[j] = wave_xor(crc[j]);
         } else {
-            lane_shift<MR>(lmat, lane, crc, v);
-        }
-#pragma unroll
-        for (int jj = 0; jj < MR; ++jj) {
-            v[jj] = wave_xor(v[jj]);
-            if (pass == 0) o_raw[jj] = v[jj];
-            else o_hi[jj] = v[jj];
+            const uint32_t t = row_totals<MR>(nib, lane, crc);
+            if (pass == 0) r_raw = t;
+            else r_hi = t;
         }
     }
-    if constexpr (kSpread && !(kFlags & 4)) {
+    if constexpr (kFlags & 4) {
+        if (passes == 1)
+#pragma unroll
+            for (int j = 0; j < MR; ++j) f_hi[j] = split && wave > o_wave ? f_raw[j] : 0u;
+        if (lane == 0)
+#pragma unroll
+            for (int j = 0; j < MR; ++j) {
+                red[0][wave][j] = f_raw[j];
+                red[1][wave][j] = f_hi[j];
+            }
+    } else {
         if (passes == 1) r_hi = split && wave > o_wave ? r_raw : 0u;
         if (lane < static_cast<uint32_t>(MR)) {
             red[0][wave][lane] = r_raw;
             red[1][wave][lane] = r_hi;
         }
-    } else {
-        if (passes == 1)
-#pragma unroll
-            for (int jj = 0; jj < MR; ++jj) o_hi[jj] = split && wave > o_wave ? o_raw[jj] : 0u;
-        if (lane == 0)
-#pragma unroll
-            for (int j = 0; j < MR; ++j) {
-                red[0][wave][j] = o_raw[j];
-                red[1][wave][j] = o_hi[j];
-            }
     }
     __syncthreads();
     // Row ends -> tile end, spread over lanes: wave 0 folds the raw values, wave 1 the hi
@@ -364,142 +259,107 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
     }
 }
 
-// One workgroup streams NT consecutive tiles of one stripe (PARTIAL: its partial last tile,
-// NT = 1, in a second tiny launch so that the masking never touches the main kernel).  The
-// slicing tables and lane matrices are staged once per workgroup, and tile t+1's loads are
-// issued into the registers the multiply of tile t has just freed, before tile t's CRC: the
-// CRC of one tile runs under the next tile's loads instead of idling the workgroup's memory
-// pipe.  sched_barrier keeps that order (left alone the compiler hoists the loads over the
-// multiply, into fresh registers).
-template <int K, int MR, int LC, bool PARTIAL, int NT>
+// One workgroup = one tile of one stripe (PARTIAL: the stripe's partial last tile, in a
+// second B-workgroup launch so that the masking never touches the main kernel).  Several
+// tiles per workgroup (constants staged once, the next tile's loads issued under this
+// tile's CRC) held 149-197 VGPRs and lost 5-7 % (r2g).
+template <int K, int MR, int LC, bool PARTIAL>
 __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     constexpr int NV = LC / 4;
     constexpr int NQ = LC / 16;
     constexpr uint32_t kRow = 64u * LC;
     constexpr uint32_t kTile = 4u * kRow;
-    __shared__ uint32_t tab[kSlice * 256 * kCopies];
-    __shared__ uint32_t lmat[kNib ? 16 * kNibStride : 32 * 64];
-    __shared__ uint32_t red[2][2][4][MR];
+    __shared__ uint32_t tab[8 * 256];
+    __shared__ uint32_t nib[kNibWords];
+    __shared__ uint32_t red[2][4][MR];
     __shared__ uint32_t wm[96];  // S_{64*LC*(3-w)}, w < 3
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint32_t b, first, count;
+    uint32_t b, tile;
     if constexpr (PARTIAL) {
         b = blockIdx.x;
-        first = a.tps - 1;
-        count = 1;
+        tile = a.tps - 1;
     } else {
-        const uint32_t gps = (a.tps_full + NT - 1) / NT;  // tile groups per stripe
         uint32_t t = blockIdx.x;
         if (a.xcd_remap) t = (t % 8u) * (gridDim.x / 8u) + t / 8u;
-        b = t / gps;
-        first = (t - b * gps) * NT;
-        count = a.tps_full - first < static_cast<uint32_t>(NT) ? a.tps_full - first : NT;
+        b = t / a.tps_full;
+        tile = t - b * a.tps_full;
     }
+    const uint64_t tile_off = static_cast<uint64_t>(tile) * kTile;
     uint8_t* stripe = a.base + static_cast<uint64_t>(b) * a.stripe_stride;
     const uint32_t in_tile = wave * kRow + lane_piece<LC>(lane);  // tile offset of piece q = 0
     // Bytes of the partial tile inside the shard (a multiple of 16).
-    const uint32_t lim = PARTIAL ? static_cast<uint32_t>(a.S - static_cast<uint64_t>(first) * kTile) : kTile;
+    const uint32_t lim = PARTIAL ? static_cast<uint32_t>(a.S - tile_off) : kTile;
     const ci32 in_idx = as_const(a.in_idx);
     const ci32 out_idx = as_const(a.out_idx);
 
-    constexpr int kFill = kSlice * 256 * kCopies / kTThreads;  // table words per thread
-    constexpr int kMWords = kNib ? 16 * kNibStride : 32 * 64;
-    constexpr int kMFill = (kMWords + kTThreads - 1) / kTThreads;  // lane-shift words per thread
-    uint32_t tv[kFill], mv[kMFill];
-    if constexpr (kFlags & 1) {
+    // Constants (L2 hits) into registers first, then the data loads: the LDS writes below
+    // wait for the constants only (in-order vmcnt).
+    constexpr int kFill = 8 * 256 / kTThreads;                          // table words per thread
+    constexpr int kNFill = (kNibWords + kTThreads - 1) / kTThreads;     // nibble-table words
+    uint32_t tv[kFill], nv[kNFill];
 #pragma unroll
-        for (int r = 0; r < kFill; ++r) tv[r] = tid * 3u + r;
+    for (int r = 0; r < kFill; ++r) tv[r] = (kFlags & 1) ? tid * 3u + r : a.tab8[tid + r * kTThreads];
 #pragma unroll
-        for (int r = 0; r < kMFill; ++r) mv[r] = tid * 5u + r;
-    } else {
-        const uint32_t* src = kSlice == 8 ? a.tab8 : &a.c->table[0][0];
-#pragma unroll
-        for (int r = 0; r < kFill; ++r) tv[r] = src[(tid + r * kTThreads) / kCopies];
-#pragma unroll
-        for (int r = 0; r < kMFill; ++r) {
-            const uint32_t i = tid + r * kTThreads;
-            mv[r] = (kMWords % kTThreads == 0 || i < kMWords) ? a.lanemat[i] : 0u;
-        }
+    for (int r = 0; r < kNFill; ++r) {
+        const uint32_t i = tid + r * kTThreads;
+        nv[r] = (kFlags & 1) ? tid * 5u + r : i < kNibWords ? a.nib[i] : 0u;
     }
     const uint32_t wmv = tid < 96u ? a.wavemat[tid] : 0u;
-    // All K inputs of a tile in flight (nontemporal: every byte is read once).
+    // All K inputs of the tile in flight (nontemporal: every byte is read once).
     uint32_t x[K][NV];
-    auto load_tile = [&](uint64_t tile_off) {
 #pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const uint8_t* p = stripe + static_cast<uint64_t>(in_idx[c]) * a.shard_stride + tile_off + in_tile;
+    for (int c = 0; c < K; ++c) {
+        const uint8_t* p = stripe + static_cast<uint64_t>(in_idx[c]) * a.shard_stride + tile_off + in_tile;
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                u32x4 v = u32x4{0u, 0u, 0u, 0u};
-                if (!PARTIAL || in_tile + 1024u * q < lim)
-                    v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q));
-                x[c][4 * q] = v.x;
-                x[c][4 * q + 1] = v.y;
-                x[c][4 * q + 2] = v.z;
-                x[c][4 * q + 3] = v.w;
-            }
+        for (int q = 0; q < NQ; ++q) {
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (!PARTIAL || in_tile + 1024u * q < lim)
+                v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q));
+            x[c][4 * q] = v.x;
+            x[c][4 * q + 1] = v.y;
+            x[c][4 * q + 2] = v.z;
+            x[c][4 * q + 3] = v.w;
         }
-    };
-    load_tile(static_cast<uint64_t>(first) * kTile);
-    // Slicing tables (L2 hits): written to LDS once their loads, issued before the data's,
-    // have landed -- the in-order vmcnt lets that wait skip the data loads.
+    }
 #pragma unroll
     for (int r = 0; r < kFill; ++r) tab[tid + r * kTThreads] = tv[r];
 #pragma unroll
-    for (int r = 0; r < kMFill; ++r) {
+    for (int r = 0; r < kNFill; ++r) {
         const uint32_t i = tid + r * kTThreads;
-        if (kMWords % kTThreads == 0 || i < kMWords) lmat[i] = mv[r];
+        if (i < kNibWords) nib[i] = nv[r];
     }
     if (tid < 96u) wm[tid] = wmv;
 
-#pragma unroll 1
-    for (uint32_t i = 0; i < count; ++i) {
-        const uint32_t tile = first + i;
-        const uint64_t tile_off = static_cast<uint64_t>(tile) * kTile;
-        if constexpr (NT > 1 && !kPrefetch)
-            if (i > 0) load_tile(tile_off);
-        uint32_t acc[MR][NV] = {};
-        {
-            cu32 tables = as_const(a.tables);
-            asm volatile("" : "+s"(tables));
+    uint32_t acc[MR][NV] = {};
+    {
+        cu32 tables = as_const(a.tables);
+        asm volatile("" : "+s"(tables));
 #pragma unroll
-            for (int c = 0; c + 1 < K; c += 2) {
-                if constexpr (kTabSeq > 0) {
-                    // The pair's coefficient loads wait for the accumulators of kTabSeq pairs
-                    // back: without it all K*MR*5 table words are loaded up front and spill
-                    // SGPRs (RS(12,5): 300 words).
-                    if (c >= 2 * kTabSeq) asm volatile("" : "+s"(tables) : "v"(acc[0][0]));
-                }
-                madd2<MR, NV>(Groups<NV>(x[c]), [&](int r) { return tables + (r * K + c) * 5; }, Groups<NV>(x[c + 1]),
-                              [&](int r) { return tables + (r * K + c + 1) * 5; }, acc, MR);
-            }
-            if constexpr (K & 1)
-                madd<MR, NV>(Groups<NV>(x[K - 1]), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, MR);
+        for (int c = 0; c + 1 < K; c += 2) {
+            if constexpr (kTabSeq > 0)
+                if (c >= 2 * kTabSeq) asm volatile("" : "+s"(tables) : "v"(acc[0][0]));
+            madd2<MR, NV>(Groups<NV>(x[c]), [&](int r) { return tables + (r * K + c) * 5; }, Groups<NV>(x[c + 1]),
+                          [&](int r) { return tables + (r * K + c + 1) * 5; }, acc, MR);
         }
-#pragma unroll
-        for (int j = 0; j < MR; ++j) {
-            uint8_t* q = stripe + static_cast<uint64_t>(out_idx[j]) * a.shard_stride + tile_off + in_tile;
-#pragma unroll
-            for (int u = 0; u < NQ; ++u)
-                if (!PARTIAL || in_tile + 1024u * u < lim)
-                    __builtin_nontemporal_store(
-                        u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
-                        reinterpret_cast<u32x4*>(q + 1024 * u));
-        }
-        if constexpr (NT > 1 && kPrefetch) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (i + 1 < count) load_tile(tile_off + kTile);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // CRC of this lane's LC contiguous parity bytes (tile offset LC * tid) per row.
-#pragma unroll
-        for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
-        if (i == 0) __syncthreads();  // tables
-        crc_tile<MR, LC>(a, acc, tab, lmat, wm, red[i & 1], tile_off, static_cast<uint64_t>(b) * a.tps + tile, tid, lane,
-                         wave);
+        if constexpr (K & 1)
+            madd<MR, NV>(Groups<NV>(x[K - 1]), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, MR);
     }
+#pragma unroll
+    for (int j = 0; j < MR; ++j) {
+        uint8_t* q = stripe + static_cast<uint64_t>(out_idx[j]) * a.shard_stride + tile_off + in_tile;
+#pragma unroll
+        for (int u = 0; u < NQ; ++u)
+            if (!PARTIAL || in_tile + 1024u * u < lim)
+                __builtin_nontemporal_store(u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
+                                            reinterpret_cast<u32x4*>(q + 1024 * u));
+    }
+    // CRC of this lane's LC contiguous parity bytes (tile offset LC * tid) per row.
+#pragma unroll
+    for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
+    __syncthreads();  // tables
+    crc_tile<MR, LC>(a, acc, tab, nib, wm, red, tile_off, static_cast<uint64_t>(b) * a.tps + tile, tid, lane, wave);
 }
 
 __device__ uint32_t shift_n(const CrcConsts* c, uint32_t r, uint64_t n) {
@@ -588,23 +448,14 @@ __global__ __launch_bounds__(256) void tile_combine_kernel(TArgs a, uint32_t log
 
 using KernelFn = void (*)(TArgs);
 
-// Tiles per workgroup in the main launch.  1: a loop over several tiles (staging amortised,
-// the next tile's loads issued before this tile's CRC) holds 149 VGPRs for RS(6,3) -> 3 waves
-// per SIMD, and measured 5-7 % slower than one tile per workgroup at 111 VGPRs / 4 waves.
-#ifndef BLBRS_ECT_NT
-#define BLBRS_ECT_NT 1
-#endif
-constexpr int kTilesPerGroup = BLBRS_ECT_NT;
-
 template <int K, bool P>
 KernelFn pick_rows(int rows) {
-    constexpr int NT = P ? 1 : kTilesPerGroup;
     switch (rows) {
-        case 1: return encode_crc_tile_kernel<K, 1, lc_for(K, 1), P, NT>;
-        case 2: return encode_crc_tile_kernel<K, 2, lc_for(K, 2), P, NT>;
-        case 3: return encode_crc_tile_kernel<K, 3, lc_for(K, 3), P, NT>;
-        case 4: return encode_crc_tile_kernel<K, 4, lc_for(K, 4), P, NT>;
-        case 5: return encode_crc_tile_kernel<K, 5, lc_for(K, 5), P, NT>;
+        case 1: return encode_crc_tile_kernel<K, 1, lc_for(K, 1), P>;
+        case 2: return encode_crc_tile_kernel<K, 2, lc_for(K, 2), P>;
+        case 3: return encode_crc_tile_kernel<K, 3, lc_for(K, 3), P>;
+        case 4: return encode_crc_tile_kernel<K, 4, lc_for(K, 4), P>;
+        case 5: return encode_crc_tile_kernel<K, 5, lc_for(K, 5), P>;
         default: return nullptr;
     }
 }
@@ -641,13 +492,9 @@ hipError_t tile_consts_for(const TileConsts** out) {
         for (int k = 1; k < 8; ++k)
             for (uint32_t i = 0; i < 256; ++i)
                 host.tab8[k][i] = (host.tab8[k - 1][i] >> 8) ^ host.tab8[0][host.tab8[k - 1][i] & 255u];
-        for (int v = 0; v < 3; ++v) {
-            const uint64_t lc = v == 0 ? 64 : v == 1 ? 32 : 16;
+        for (int v = 0; v < 2; ++v) {
+            const uint64_t lc = v == 0 ? 32 : 16;
             uint32_t col[32];
-            for (int l = 0; l < 64; ++l) {
-                crc_shift_matrix(lc * static_cast<uint64_t>(63 - l), col);
-                for (int i = 0; i < 32; ++i) host.lanemat[v][i][l] = col[i];
-            }
             for (int w = 0; w < 4; ++w) {
                 crc_shift_matrix(64 * lc * static_cast<uint64_t>(3 - w), col);
                 for (int i = 0; i < 32; ++i) host.wavemat[v][w][i] = col[i];
@@ -724,16 +571,16 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     a.block = in.block < in.S + in.phase ? in.block : in.S + in.phase;
     a.seeds = in.seeds;
     a.B = in.B;
-    const uint32_t log2t = lc == 64 ? 14u : lc == 32 ? 13u : 12u;
+    const uint32_t log2t = lc == 32 ? 13u : 12u;
     a.tps = static_cast<uint32_t>((in.S + (uint64_t{1} << log2t) - 1) >> log2t);
     a.tps_full = static_cast<uint32_t>(in.S >> log2t);
     a.nblocks = static_cast<uint32_t>((in.S + a.phase + a.block - 1) / a.block);
     a.c = c;
-    a.lanemat = kNib ? &tc->nib[lc_index(lc)][0] : &tc->lanemat[lc_index(lc)][0][0];
+    a.nib = &tc->nib[lc_index(lc)][0];
     a.wavemat = &tc->wavemat[lc_index(lc)][0][0];
     a.tab8 = &tc->tab8[0][0];
     const uint64_t tiles = static_cast<uint64_t>(in.B) * a.tps;
-    const uint64_t groups = static_cast<uint64_t>(in.B) * ((a.tps_full + kTilesPerGroup - 1) / kTilesPerGroup);
+    const uint64_t groups = static_cast<uint64_t>(in.B) * a.tps_full;  // one tile per workgroup
     a.xcd_remap = groups % 8 == 0 ? 1u : 0u;
     const uint64_t nraw = static_cast<uint64_t>(in.rows) * tiles;
     uint32_t* buf = nullptr;
