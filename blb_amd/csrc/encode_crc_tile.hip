@@ -11,12 +11,12 @@
 //    tiles -- rs_code_kernel's grid.  Wave w owns the tile's w-th 64*LC-byte row, loaded
 //    and stored with coalesced 1 KiB instructions (lane_piece) and transposed in registers
 //    (lane_contiguous) so that lane L holds the LC contiguous bytes at tile offset LC * tid.
-//  * CRC: each lane runs one slicing-by-4 chain per parity row over its LC bytes (tables in
-//    LDS; C interleaved copies would spread bank conflicts but cost more to stage, so C = 1),
-//    shifts it to its wave row's end with its own matrix S_{LC*(63-lane)} (64 matrices
-//    staged in LDS), and the wave XORs its lanes; one lane per row shifts the 4 row values to the tile end (S_{64*LC*(3-w)}) and
-//    XORs them.  Per workgroup that is 4*C + 8 KiB of constants from L2 -- kept small
-//    because every workgroup stages them for one tile.
+//  * CRC: each lane runs one slicing-by-8 chain per parity row over its LC bytes (8 KiB of
+//    tables in LDS).  The lane's chains are shifted to the row end by S_{LC*(63-lane)} in two
+//    nibble-table factors (8.5 KiB in LDS), the first on every row, the second on one row
+//    per lane after an 8-lane XOR (row_totals); the row totals are then folded to the tile
+//    end with S_{64*LC*(3-w)}, spread over the lanes of waves 0 and 1.  Every workgroup
+//    stages 17 KiB of constants from L2 for its one tile.
 //  * Tiles ignore block boundaries.  A tile that contains one (at dword offset o) also runs
 //    a second chain over its bytes at offsets >= o only (`hi`); by linearity the part before
 //    the boundary is raw ^ hi.  A combine kernel then Horner-folds each block's tiles and
