@@ -438,3 +438,33 @@ def test_reconstruct_and_verify_fused(oracle_lib):
         pinned = [None if i == 0 else torch.from_numpy(full[i].copy()).pin_memory().numpy() for i in range(k + m)]
         assert enc.ReconstructAndVerify(pinned)   # zero-copy variant
         assert np.array_equal(pinned[0], full[0])
+
+
+# ---------------------------------------------------------------- SURVEY §8(d) edge fixtures
+
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (10, 4), (12, 5)])
+@pytest.mark.parametrize("fill", [0x00, 0xFF])
+def test_constant_data_edge_fixtures(oracle_lib, dev, k, m, fill):
+    """All-0x00 / all-0xFF data at the §8(d) edge lengths: host Encode and device EncodeBatch
+    equal the oracle (all-zero data -> all-zero parity; all-0xFF -> one constant per row),
+    and a 2-erasure Reconstruct restores the data."""
+    enc = rs.New(k, m)
+    for S in (1, 15, 12000, 20000, 98765, 123000):
+        data = [np.full(S, fill, np.uint8) for _ in range(k)]
+        want = oracle_encode(oracle_lib, k, m, data)
+        if fill == 0:
+            assert all(not w.any() for w in want)
+        else:
+            assert all(np.all(w == w[0]) for w in want)
+        sh = [d.copy() for d in data] + [np.full(S, 0x5A, np.uint8) for _ in range(m)]
+        enc.Encode(sh)
+        for j in range(m):
+            assert np.array_equal(sh[k + j], want[j]), (k, m, fill, S, j)
+        st = torch.from_numpy(np.stack(data + [np.full(S, 0xA5, np.uint8)] * m)[None]).to(dev)
+        enc.EncodeBatch(st)
+        got = st[0, k:].cpu().numpy()
+        for j in range(m):
+            assert np.array_equal(got[j], want[j]), (k, m, fill, S, j, "dev")
+        cur = [None if i in (0, k - 1) else sh[i].copy() for i in range(k + m)]
+        enc.Reconstruct(cur)
+        assert all(np.array_equal(cur[i], sh[i]) for i in range(k + m)), (k, m, fill, S)
