@@ -33,8 +33,9 @@ bool encode_crc_supported(const EncodeCrcArgs& a);
 // BLBRS_EC_PERSISTENT=1 forces the segment kernel (A/B measurements).
 hipError_t launch_encode_crc(const EncodeCrcArgs& a, hipStream_t stream);
 
-// The tile-grid form: rows <= 4, 16-byte aligned base and strides, S a multiple of 16 (the
-// last tile may be partial), block >= the 8 KiB tile, block and phase multiples of 4.
+// The tile-grid form: k in {3, 4, 6, 8, 10, 12} and rows <= 5, 16-byte aligned base and
+// strides, S a multiple of 16 (the last tile may be partial), block >= the tile (4 or 8 KiB),
+// block and phase multiples of 4.
 bool encode_crc_tile_supported(const EncodeCrcArgs& a);
 hipError_t launch_encode_crc_tile(const EncodeCrcArgs& a, hipStream_t stream);
 
