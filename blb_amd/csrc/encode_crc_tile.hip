@@ -52,11 +52,16 @@ constexpr uint64_t kOrd = 0x7FFFFFFFull;            // S_{kOrd} = I (checked on 
 #endif
 constexpr int kFlags = BLBRS_ECT_FLAGS;
 
-// Lane chunks: LC = 32 bytes (8 KiB tiles) for every shape but the widest, 16 bytes (4 KiB
-// tiles) when k + rows >= 17: half the input registers (RS(12,5) at 32-byte chunks needs 256
-// VGPRs, 25.4 vs 16.8 ms at the time), twice the lane shifts per byte.  RS(10,4) is faster at
-// 32 (11.4 vs 12.7 ms).  64-byte chunks (16 KiB tiles, 2 waves per SIMD) were slower.
-constexpr int lc_for(int k, int rows) { return k + rows >= 17 ? 16 : 32; }
+// Lane chunks: LC = 32 bytes (8 KiB tiles) for every instantiated shape.  16-byte chunks
+// (4 KiB tiles) halve the input registers at twice the lane shifts per byte; RS(12,5) needed
+// them while its 32-byte form took 256 VGPRs, and since the shift work moved to row_totals
+// and the coefficient loads were sequenced it fits 168 and runs 14.10-14.15 vs 15.06-15.11 ms
+// (r2u_lc32).  k + rows >= BLBRS_ECT_LC16_MIN selects 16 (A/B builds).  64-byte chunks (16
+// KiB tiles, 2 waves per SIMD) were slower.
+#ifndef BLBRS_ECT_LC16_MIN
+#define BLBRS_ECT_LC16_MIN 18
+#endif
+constexpr int lc_for(int k, int rows) { return k + rows >= BLBRS_ECT_LC16_MIN ? 16 : 32; }
 constexpr int lc_index(int lc) { return lc == 32 ? 0 : 1; }
 
 // Per LC: the nibble tables of the lane shifts and the row-end -> tile-end matrices.
