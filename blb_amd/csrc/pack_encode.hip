@@ -11,12 +11,14 @@
 //
 // Per (tile, piece) the extent layout is uniform over the workgroup:
 //  * ZERO  -- no extent overlaps the tile (a hole or the pad, store.go:974-980);
-//  * COPY  -- one extent covers the whole tile: each lane reads the aligned 16-byte source
-//    block(s) holding its 16 bytes and realigns them with v_alignbyte (the source
-//    misalignment is uniform: tile offsets step by 16), every load issued before any use;
+//  * COPY  -- one extent covers the whole tile: each lane reads the aligned 16-byte block
+//    holding the start of its 16 bytes, takes the following block from the next lane (DPP
+//    rotate) and realigns the pair with v_alignbyte (the source misalignment is uniform: tile
+//    offsets step by 16); every load of every COPY piece is issued before any use;
 //  * MIXED -- an extent starts or ends inside the tile (tract boundaries, a partial last
-//    tile): the tile is assembled byte by byte in LDS, then read back.  Rare: about two
-//    tiles per piece for multi-MiB tracts.
+//    tile): each lane resolves its own 16 bytes from the extents (one extent: funnel with a
+//    per-lane shift; a hole: zero; cut by a boundary: bytes).  Other pieces of the same tile
+//    stay COPY / ZERO.  Rare: about two tiles per piece for multi-MiB tracts.
 // Reads of a source never leave the bytes of its extent's 16-byte blocks that hold wanted
 // bytes (pack.hip's rule), so no read touches a page the source does not own.
 #include "pack.hpp"
@@ -102,6 +104,17 @@ __device__ __forceinline__ V4 funnel(const V4& a, const V4& b, uint32_t q, uint3
     }
 }
 
+// The same with a per-lane shift s (MIXED pieces): dword select by q, then v_alignbyte by r.
+__device__ __forceinline__ V4 funnel_lane(const V4& a, const V4& b, uint32_t s) {
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const uint32_t q = s >> 2, r = s & 3u;
+    uint32_t d[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) d[i] = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
+    return V4{__builtin_amdgcn_alignbyte(d[1], d[0], r), __builtin_amdgcn_alignbyte(d[2], d[1], r),
+              __builtin_amdgcn_alignbyte(d[3], d[2], r), __builtin_amdgcn_alignbyte(d[4], d[3], r)};
+}
+
 __device__ __forceinline__ V4 ldnt(const uint8_t* p) {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     return V4{v.x, v.y, v.z, v.w};
@@ -121,27 +134,68 @@ __device__ __forceinline__ void store_part(uint8_t* p, const V4& v, uint32_t n) 
     for (uint32_t j = 0; j < n; ++j) p[j] = static_cast<uint8_t>(w[j >> 2] >> (8 * (j & 3)));
 }
 
+// Lane i receives lane (i + 1) mod 64's dword (DPP wave_rol:1, no LDS).
+__device__ __forceinline__ uint32_t rol1(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x134, 0xF, 0xF, false));
+}
+__device__ __forceinline__ V4 rol1(const V4& v) { return V4{rol1(v.x), rol1(v.y), rol1(v.z), rol1(v.w)}; }
+
+// Bytes [c0, c0 + 16) of a piece whose tile is MIXED, resolved by this lane alone from the
+// piece's extents (e = the tile's first extent ending past the tile start, hi = the piece's
+// end in the table).  A chunk inside one extent is two aligned loads and a per-lane funnel, a
+// chunk inside a hole or past t1 is zero (bytes past t1 are never stored), and a chunk that
+// an extent boundary cuts is assembled byte by byte.  Reads stay within wanted 16-byte blocks.
+__device__ V4 mixed_chunk(const uint64_t* ex, uint64_t e, uint64_t hi, uint64_t c0, uint64_t t1) {
+    while (e < hi && ex[4 * e + 1] + ex[4 * e + 2] <= c0) ++e;
+    const uint64_t c1 = c0 + 16 < t1 ? c0 + 16 : t1;
+    if (c0 >= t1 || e >= hi || ex[4 * e + 1] >= c1) return V4{0u, 0u, 0u, 0u};
+    const uint64_t off = ex[4 * e + 1], len = ex[4 * e + 2];
+    if (off <= c0 && off + len >= c0 + 16) {
+        const uint64_t s = ex[4 * e] + (c0 - off);
+        const uint32_t mis = static_cast<uint32_t>(s & 15u);
+        const uint8_t* sa = reinterpret_cast<const uint8_t*>(s - mis);
+        const V4 lo = ldnt(sa);
+        if (mis == 0) return lo;
+        return funnel_lane(lo, ldnt(sa + 16), mis);
+    }
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint64_t pos = c0 + j;
+        if (pos >= t1) break;
+        while (e < hi && ex[4 * e + 1] + ex[4 * e + 2] <= pos) ++e;
+        if (e < hi && ex[4 * e + 1] <= pos) {
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(ex[4 * e]);
+            w[j >> 2] |= static_cast<uint32_t>(src[pos - ex[4 * e + 1]]) << (8 * (j & 3));
+        }
+    }
+    return V4{w[0], w[1], w[2], w[3]};
+}
+
+// One workgroup per (stripe, tile); wave w owns the tile's bytes [w*U KiB, (w+1)*U KiB) of
+// every piece, chunk u of lane l at w*U KiB + u KiB + 16 l, so the 16-byte block after lane
+// 63's chunk u is lane 0's chunk u + 1 (a DPP rotate away) except after the last chunk.
 template <int K, int MR, int U>
 __global__ __launch_bounds__(kPEThreads) void pack_encode_kernel(PEArgs a) {
-    constexpr uint32_t kStep = kPEThreads * 16u;  // 4 KiB per chunk row
-    constexpr uint32_t kTile = kStep * U;
+    constexpr uint32_t kWaveRow = 64u * 16u;             // 1 KiB per wave instruction
+    constexpr uint32_t kWaveRun = kWaveRow * U;          // contiguous bytes per wave
+    constexpr uint32_t kTile = kWaveRun * (kPEThreads / 64u);
     constexpr int NV = 4 * U;
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kTile];
 
     const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
     uint32_t t = blockIdx.x;
     if (a.xcd_remap) t = (t % 8u) * (gridDim.x / 8u) + t / 8u;
     const uint32_t b = t / a.tps;
     const uint64_t t0 = static_cast<uint64_t>(t - b * a.tps) * kTile;
     const uint64_t t1 = t0 + kTile < a.S ? t0 + kTile : a.S;
     const bool full = t1 - t0 == kTile;
+    const uint64_t lane_off = t0 + (tid >> 6) * kWaveRun + 16u * lane;  // + u KiB
     uint8_t* stripe = a.base + static_cast<uint64_t>(b) * a.stripe_stride;
     const uint64_t* ex = a.table + static_cast<uint64_t>(a.B) * K + 1;
 
     // Per piece, the tile's extent layout (uniform, from the pre-pass): lane p of every
     // wave loads piece p's descriptor -- K loads in parallel -- and the values are read back
     // per piece with v_readlane.
-    const uint32_t lane = tid & 63u;
     uint32_t my_kind = kZero;
     uint64_t my_first = 0, my_sbase = 0;
     if (lane < static_cast<uint32_t>(K)) {
@@ -155,133 +209,108 @@ __global__ __launch_bounds__(kPEThreads) void pack_encode_kernel(PEArgs a) {
         const uint32_t hi32 = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l);
         return (static_cast<uint64_t>(hi32) << 32) | lo32;
     };
-    uint32_t copy_mask = 0, zero_mask = 0;
+    uint32_t kinds = 0;  // 2 bits per piece
+#pragma unroll
+    for (int p = 0; p < K; ++p) kinds |= __builtin_amdgcn_readlane(my_kind, p) << (2 * p);
+    auto kind = [&](int p) { return (kinds >> (2 * p)) & 3u; };
+
+    // COPY loads of every piece in flight before any use: the aligned 16-byte blocks of the
+    // wave's run, plus (lane 63 only, misaligned sources only) the block just past it.
+    V4 lo_blk[K][U], tail[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) {
-        const uint32_t kd = __builtin_amdgcn_readlane(my_kind, p);
-        copy_mask |= (kd == kCopy ? 1u : 0u) << p;
-        zero_mask |= (kd == kZero ? 1u : 0u) << p;
+        if (kind(p) != kCopy) continue;
+        const uint64_t sb = rl64(my_sbase, p) + lane_off;
+        const uint32_t mis = static_cast<uint32_t>(sb & 15u);
+        const uint8_t* sa = reinterpret_cast<const uint8_t*>(sb - mis);
+#pragma unroll
+        for (int u = 0; u < U; ++u) lo_blk[p][u] = ldnt(sa + u * kWaveRow);
+        if (mis != 0 && lane == 63u) tail[p] = ldnt(sa + (U - 1) * kWaveRow + 16);
     }
+
     uint32_t acc[MR][NV] = {};
     cu32 tables = as_const(a.tables);
     asm volatile("" : "+s"(tables));
-    // Store the packed data piece p (every byte written: PackTracts zero-fills,
-    // store.go:974-980) and multiply it into the parity rows.
-    auto consume = [&](int p, const V4 (&x)[U]) {
-        uint8_t* dp = stripe + static_cast<uint64_t>(p) * a.shard_stride + t0 + 16u * tid;
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        V4 x[U];
+        const uint32_t kd = kind(p);
+        if (kd == kZero) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = V4{0u, 0u, 0u, 0u};
+        } else if (kd == kCopy) {
+            const uint32_t mis = static_cast<uint32_t>((rl64(my_sbase, p) + lane_off) & 15u);
+            if (mis == 0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[u] = lo_blk[p][u];
+            } else {
+                V4 nb[U];  // lane l: the block after lane l's chunk u (lane 63: chunk u+1 of lane 0)
+#pragma unroll
+                for (int u = 0; u < U; ++u) nb[u] = rol1(lo_blk[p][u]);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const V4 h63 = u + 1 < U ? nb[u + 1] : tail[p];
+                    const V4 hb = lane == 63u ? h63 : nb[u];
+                    x[u] = funnel(lo_blk[p][u], hb, mis >> 2, mis & 3u);
+                }
+            }
+        } else {
+            const uint64_t piece = static_cast<uint64_t>(b) * K + p;
+            const uint64_t hi = a.table[piece + 1];
+            const uint64_t first = rl64(my_first, p);
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = mixed_chunk(ex, first, hi, lane_off + u * kWaveRow, t1);
+        }
+        // Store the packed data piece p (every byte written: PackTracts zero-fills,
+        // store.go:974-980) and multiply it into the parity rows.
+        uint8_t* dp = stripe + static_cast<uint64_t>(p) * a.shard_stride + lane_off;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t c0 = t0 + u * kStep + 16u * tid;
-            if (full) stnt(dp + u * kStep, x[u]);
-            else if (c0 < t1) store_part(dp + u * kStep, x[u], static_cast<uint32_t>(t1 - c0));
+            const uint64_t c0 = lane_off + u * kWaveRow;
+            if (full) stnt(dp + u * kWaveRow, x[u]);
+            else if (c0 < t1) store_part(dp + u * kWaveRow, x[u], static_cast<uint32_t>(t1 - c0));
         }
         uint32_t xv[NV];
 #pragma unroll
         for (int u = 0; u < U; ++u) unpack(x[u], xv + 4 * u);
         madd<MR, NV>(Groups<NV>(xv), [&](int r) { return tables + (r * K + p) * 5; }, acc, static_cast<int>(a.rows));
-    };
-    const bool any_mixed = (copy_mask | zero_mask) != (1u << K) - 1u;
-
-    if (!any_mixed) {
-        // Fast path: COPY loads of every piece in flight before any use.
-        V4 lo_blk[K][U], hi_blk[K][U];
-#pragma unroll
-        for (int p = 0; p < K; ++p) {
-            if (!((copy_mask >> p) & 1u)) continue;
-            const uint64_t sb = rl64(my_sbase, p) + t0 + 16u * tid;
-            const uint32_t mis = static_cast<uint32_t>(sb & 15u);
-            const uint8_t* sa = reinterpret_cast<const uint8_t*>(sb - mis);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                lo_blk[p][u] = ldnt(sa + u * kStep);
-                hi_blk[p][u] = mis ? ldnt(sa + u * kStep + 16) : lo_blk[p][u];  // holds wanted bytes
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < K; ++p) {
-            V4 x[U];
-            const uint32_t mis = static_cast<uint32_t>((rl64(my_sbase, p) + t0) & 15u);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                x[u] = ((zero_mask >> p) & 1u) ? V4{0u, 0u, 0u, 0u}
-                       : mis            ? funnel(lo_blk[p][u], hi_blk[p][u], mis >> 2, mis & 3u)
-                                        : lo_blk[p][u];
-            consume(p, x);
-        }
-    } else {
-        // Slow path (an extent starts or ends inside the tile, or a partial last tile): each
-        // piece's [t0, t1) assembled byte by byte in LDS from its extents, then read back.
-        // The barriers are unconditional here: every thread runs every piece.
-#pragma unroll 1
-        for (int p = 0; p < K; ++p) {
-            __syncthreads();  // the previous piece's reads of `stage` are done
-            const uint64_t piece = static_cast<uint64_t>(b) * K + p;
-            const uint64_t hi = a.table[piece + 1];
-            const uint64_t first = rl64(my_first, p);
-            uint64_t cur = t0;
-            for (uint64_t e = first; cur < t1;) {
-                const uint64_t off = e < hi ? ex[4 * e + 1] : t1;
-                uint64_t end;
-                if (off <= cur) {  // inside extent e
-                    end = off + ex[4 * e + 2] < t1 ? off + ex[4 * e + 2] : t1;
-                    const uint8_t* src = reinterpret_cast<const uint8_t*>(ex[4 * e]) + (cur - off);
-                    for (uint64_t i = tid; i < end - cur; i += kPEThreads) stage[cur - t0 + i] = src[i];
-                    ++e;
-                } else {  // hole or pad up to the next extent / tile end
-                    end = off < t1 ? off : t1;
-                    for (uint64_t i = tid; i < end - cur; i += kPEThreads) stage[cur - t0 + i] = 0;
-                }
-                cur = end > cur ? end : cur;
-            }
-            for (uint64_t i = t1 - t0 + tid; i < kTile; i += kPEThreads) stage[i] = 0;
-            __syncthreads();
-            V4 x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = *reinterpret_cast<const V4*>(stage + u * kStep + 16u * tid);
-            // consume() with a runtime p: the table index is the only p-dependent part.
-            uint8_t* dp = stripe + static_cast<uint64_t>(p) * a.shard_stride + t0 + 16u * tid;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint64_t c0 = t0 + u * kStep + 16u * tid;
-                if (full) stnt(dp + u * kStep, x[u]);
-                else if (c0 < t1) store_part(dp + u * kStep, x[u], static_cast<uint32_t>(t1 - c0));
-            }
-            uint32_t xv[NV];
-#pragma unroll
-            for (int u = 0; u < U; ++u) unpack(x[u], xv + 4 * u);
-            madd<MR, NV>(Groups<NV>(xv), [&](int r) { return tables + (r * K + p) * 5; }, acc,
-                         static_cast<int>(a.rows));
-        }
     }
     const ci32 out_idx = as_const(a.out_idx);
 #pragma unroll
     for (int r = 0; r < MR; ++r) {
         if (r >= static_cast<int>(a.rows)) break;
-        uint8_t* q = stripe + static_cast<uint64_t>(out_idx[r]) * a.shard_stride + t0 + 16u * tid;
+        uint8_t* q = stripe + static_cast<uint64_t>(out_idx[r]) * a.shard_stride + lane_off;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t c0 = t0 + u * kStep + 16u * tid;
-            if (full) stnt(q + u * kStep, pack(acc[r] + 4 * u));
-            else if (c0 < t1) store_part(q + u * kStep, pack(acc[r] + 4 * u), static_cast<uint32_t>(t1 - c0));
+            const uint64_t c0 = lane_off + u * kWaveRow;
+            if (full) stnt(q + u * kWaveRow, pack(acc[r] + 4 * u));
+            else if (c0 < t1) store_part(q + u * kWaveRow, pack(acc[r] + 4 * u), static_cast<uint32_t>(t1 - c0));
         }
     }
 }
 
 using KernelFn = void (*)(PEArgs);
 
-#ifndef BLBRS_PE_U
-#define BLBRS_PE_U 1
+// 16-byte chunks per lane per piece (tile = 4 KiB * U), measured (tools/pe_variants.sh,
+// profiles/r02/pack_encode_ab/): RS(6,3) B=1024 U=1/2/4 20.2/19.8/20.4 ms (22.3 ms for the
+// previous LDS-assembly kernel at U=1); RS(12,5) B=512 U=1/2/4 23.7/24.0/46.6 ms.
+#ifndef BLBRS_PE_U_NARROW
+#define BLBRS_PE_U_NARROW 2
 #endif
-constexpr int kU = BLBRS_PE_U;  // 16-byte chunks per lane per piece (tile = 4 KiB * kU)
+#ifndef BLBRS_PE_U_WIDE
+#define BLBRS_PE_U_WIDE 1
+#endif
+constexpr int pe_u(uint32_t k) { return k <= 6 ? BLBRS_PE_U_NARROW : BLBRS_PE_U_WIDE; }
 
 template <int K>
 KernelFn pick_rows(uint32_t rows) {
+    constexpr int U = pe_u(K);
     switch (rows) {
-        case 1: return pack_encode_kernel<K, 1, kU>;
-        case 2: return pack_encode_kernel<K, 2, kU>;
-        case 3: return pack_encode_kernel<K, 3, kU>;
-        case 4: return pack_encode_kernel<K, 4, kU>;
-        case 5: return pack_encode_kernel<K, 5, kU>;
+        case 1: return pack_encode_kernel<K, 1, U>;
+        case 2: return pack_encode_kernel<K, 2, U>;
+        case 3: return pack_encode_kernel<K, 3, U>;
+        case 4: return pack_encode_kernel<K, 4, U>;
+        case 5: return pack_encode_kernel<K, 5, U>;
         default: return nullptr;
     }
 }
@@ -305,7 +334,7 @@ KernelFn pick(uint32_t k, uint32_t rows) {
 bool pack_encode_supported(const PackEncodeArgs& a) {
     const bool aligned = (reinterpret_cast<uintptr_t>(a.base) & 15u) == 0 && (a.shard_stride & 15u) == 0 &&
                          (a.stripe_stride & 15u) == 0;
-    const uint64_t tile = 4096ull * kU;
+    const uint64_t tile = 4096ull * pe_u(a.k);
     return a.base && aligned && pick(a.k, a.rows) != nullptr && a.nextents <= 0xFFFFFFFFull &&
            static_cast<uint64_t>(a.B) * ((a.S + tile - 1) / tile) <= 0x7FFFFFFFull;
 }
@@ -313,7 +342,7 @@ bool pack_encode_supported(const PackEncodeArgs& a) {
 hipError_t launch_pack_encode(const PackEncodeArgs& in, hipStream_t stream) {
     if (in.B == 0 || in.S == 0) return hipSuccess;
     if (!pack_encode_supported(in)) return hipErrorInvalidValue;
-    const uint64_t tile = 4096ull * kU;
+    const uint64_t tile = 4096ull * pe_u(in.k);
     const uint64_t ndesc = static_cast<uint64_t>(in.B) * in.k * ((in.S + tile - 1) / tile);
     if (ndesc > 0xFFFFFFFFull * 256) return hipErrorInvalidValue;
     PEArgs a{};
