@@ -49,6 +49,43 @@ __global__ __launch_bounds__(256) void mixed_kernel(uint8_t* base, uint32_t B) {
     }
 }
 
+// Store with explicit gfx950 cache-policy bits (vector stores only).
+template <int SP>
+__device__ __forceinline__ void st_pol(uint8_t* p, u32x4 v) {
+    if constexpr (SP == 0) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 4) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+constexpr const char* kPolName[6] = {"plain", "nt", "sc1", "sc1 nt", "sc0 sc1", "sc0 sc1 nt"};
+
+// The shipped grid's access pattern with store policy SP and nontemporal (LNT) or plain loads.
+template <int SP, bool LNT>
+__global__ __launch_bounds__(256) void policy_kernel(uint8_t* base, uint32_t B) {
+    constexpr int U = 4;
+    const uint32_t tps = S / (kStep * U);
+    const uint32_t total = B * tps;
+    const uint32_t t = (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u;
+    if (t >= total) return;
+    const uint32_t b = t / tps;
+    uint8_t* s = base + b * 9 * S + static_cast<uint64_t>(t - b * tps) * kStep * U + threadIdx.x * 16;
+    u32x4 x[6][U];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[r][u] = LNT ? ld(s + r * S + u * kStep) : *reinterpret_cast<const u32x4*>(s + r * S + u * kStep);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const u32x4 a = x[0][u] ^ x[1][u] ^ x[2][u];
+        const u32x4 c = x[3][u] ^ x[4][u] ^ x[5][u];
+        st_pol<SP>(s + 6 * S + u * kStep, a ^ c);
+        st_pol<SP>(s + 7 * S + u * kStep, a);
+        st_pol<SP>(s + 8 * S + u * kStep, c);
+    }
+}
+
 __device__ __forceinline__ void wait_window(uint64_t period, uint64_t lo, uint64_t hi) {
     // Spin (sleeping) until clock mod period is in [lo, hi).  Terminates: the clock runs.
     for (;;) {
@@ -121,6 +158,19 @@ int main(int argc, char** argv) {
 
     auto report = [&](const char* tag, double ms) { printf("%-48s %8.3f ms %8.1f GB/s\n", tag, ms, alg / ms / 1e6); fflush(stdout); };
     char tag[128];
+    if (argc > 2) {  // phase_probe B policy: store cache-policy A/B on the encode's pattern
+        const uint32_t g4 = (B * (S / (kStep * 4)) + 7) & ~7u;
+        for (int rep = 0; rep < 3; ++rep) {
+            printf("# policy rep %d\n", rep);
+            report("mixed U=4 builtin nt loads + nt stores", time_ms([&] { hipLaunchKernelGGL(mixed_kernel<4>, dim3(g4), dim3(256), 0, 0, base, B); }));
+#define POL(SP, L) snprintf(tag, sizeof tag, "policy stores=%s loads=%s", kPolName[SP], L ? "nt" : "plain"); \
+            report(tag, time_ms([&] { hipLaunchKernelGGL((policy_kernel<SP, L>), dim3(g4), dim3(256), 0, 0, base, B); }));
+            POL(0, true) POL(1, true) POL(2, true) POL(3, true) POL(4, true) POL(5, true) POL(1, false) POL(0, false)
+#undef POL
+        }
+        CK(hipFree(base));
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         printf("# rep %d\n", rep);
         const uint32_t g4 = (B * (S / (kStep * 4)) + 7) & ~7u;

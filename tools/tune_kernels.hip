@@ -187,10 +187,11 @@ static void stride_probe(CodeArgs a) {
 
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "zc") { zero_copy_probe(); return 0; }
+    const bool ntab = argc > 1 && std::string(argv[1]) == "nt";
     const bool stride = argc > 1 && std::string(argv[1]) == "stride";
     const bool pmc = argc > 1 && std::string(argv[1]) == "pmc";
     const bool ceil = argc > 1 && std::string(argv[1]) == "ceil";
-    if (argc > 1 && !pmc && !stride && !ceil) B = static_cast<uint32_t>(atoi(argv[1]));
+    if (argc > 1 && !pmc && !stride && !ceil && !ntab) B = static_cast<uint32_t>(atoi(argv[1]));
     const size_t total = size_t(B) * 9 * S;
     CK(hipMalloc(&g_base, total));
     CK(hipMalloc(&g_sink, 64));
@@ -241,6 +242,18 @@ int main(int argc, char** argv) {
         CK(hipDeviceSynchronize());
         printf("pmc launches done: read_bytes=%.0f copy_bytes=%.0f+%.0f rs63_bytes=%.0f+%.0f\n", double(B) * 9 * S,
                double(B) * S, double(B) * S, double(B) * 6 * S, double(B) * 3 * S);
+        return 0;
+    }
+    if (ntab) {
+        // Cache policy of the shipped grid (one tile per block, XCD remap, U = 4): NT bit 0 =
+        // nontemporal loads, bit 1 = nontemporal stores.  Plain stores land in L2 / MALL.
+        for (int rep = 0; rep < 3; ++rep) {
+            printf("# nt rep %d\n", rep);
+            run_rs<4, 3>(a, 1, "nt3", 1);
+            run_rs<4, 1>(a, 1, "nt1", 1);
+            run_rs<4, 2>(a, 1, "nt2", 1);
+            run_rs<4, 0>(a, 1, "nt0", 1);
+        }
         return 0;
     }
     if (ceil) {
