@@ -234,7 +234,7 @@ struct EncoderCore {
 struct blbrs_encoder {
     std::shared_ptr<EncoderCore> core;
     int k = 0, m = 0;
-    std::atomic<blbrs_batcher*> batcher{nullptr};  // routes host Reconstruct[Data] (blbrs_encoder_set_batcher)
+    std::atomic<blbrs_batcher*> batcher{nullptr};  // routes host Encode / Reconstruct[Data] (blbrs_encoder_set_batcher)
     std::mutex dev_mu;
     std::vector<int> devices;   // explicit list, or empty until the default list is resolved
     bool resolved = false;
@@ -499,11 +499,13 @@ std::vector<uint8_t> present_vec(const blbrs_encoder* enc, const uint8_t* presen
     return p;
 }
 
-// ---- batched host reconstructs ----
+// ---- batched host calls ----
 //
 // client/blb/reconstruct.go:65-195 calls ReconstructData once per degraded read, on one
-// stripe of `length`-byte pieces; MaxInFlight (:19,35-45) lets many run at once.  Alone,
-// each call is a launch plus a stream round trip for a few KiB..MiB of work.  A batcher
+// stripe of `length`-byte pieces; MaxInFlight (:19,35-45) lets many run at once.  The
+// tractserver runs one RSEncode per control RPC (up to RejectCtlReqThreshold = 1000 at once,
+// internal/tractserver/config.go:91), each an Encode per 4 MiB increment (store.go:1099).
+// Alone, each call is a launch plus a stream round trip for a few KiB..MiB of work.  A batcher
 // collects the calls that arrive within `window_us` (or until `max_batch` are waiting) and
 // runs them as ONE launch per (shape, erasure pattern, length) group over a device pointer
 // table, with one stream sync for the whole batch.  Each device has a queue drained by two
@@ -620,7 +622,7 @@ struct blbrs_batcher {
                 if (rc == BLBRS_OK) launches.fetch_add(1);
                 // The table is rewritten by the next group: wait for this one's launch.
                 const hipError_t e = hipStreamSynchronize(lane->stream);
-                if (rc == BLBRS_OK && e != hipSuccess) rc = hip_fail(e, "batched reconstruct");
+                if (rc == BLBRS_OK && e != hipSuccess) rc = hip_fail(e, "batched call");
             }
             for (BatchReq* r : reqs) {
                 r->rc = rc;
@@ -670,9 +672,10 @@ struct blbrs_batcher {
 
 namespace {
 
-// The host Reconstruct / ReconstructData of one stripe through `b` (blocking).  `hp` is
-// the decode plan with at least one output; argument checks have been done.
-int batched_reconstruct(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key,
+// The host Encode / Reconstruct / ReconstructData of one stripe through `b` (blocking).  `hp`
+// is the encode or decode plan (at least one output), `key` its cache key; argument checks
+// have been done.
+int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key,
                         std::shared_ptr<HostPlan> hp, uint8_t* const* shards, size_t S) {
     const int n = enc->k + enc->m;
     BatchReq req;
@@ -846,6 +849,7 @@ int blbrs_encode(blbrs_encoder* enc, uint8_t* const* shards, const size_t* lens)
     for (int i = 0; i < n; ++i)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     auto hp = enc->encode_plan();
+    if (blbrs_batcher* b = enc->batcher.load()) return batched_call(b, enc, "E", hp, shards, S);
     return host_call(enc, {Step{"E", hp.get(), Mode::kStore}}, shards, S, nullptr);
 }
 
@@ -890,7 +894,7 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "missing shard has no output buffer");
     blbrs_batcher* b = verify_ok ? nullptr : enc->batcher.load();
     if (b && !hp->out_idx.empty()) {
-        if ((rc = batched_reconstruct(b, enc, plan_key(false, present, data_only), hp, shards, S))) return rc;
+        if ((rc = batched_call(b, enc, plan_key(false, present, data_only), hp, shards, S))) return rc;
         for (int32_t i : hp->out_idx) lens[i] = S;
         return BLBRS_OK;
     }

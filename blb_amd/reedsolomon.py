@@ -133,8 +133,9 @@ class Encoder:
             self._h = None
 
     def SetBatcher(self, batcher: Optional["Batcher"]) -> None:
-        """Route this encoder's host Reconstruct / ReconstructData calls through `batcher`
-        (None detaches).  Results and errors are unchanged; concurrent callers share launches."""
+        """Route this encoder's host Encode / Reconstruct / ReconstructData calls through
+        `batcher` (None detaches).  Results and errors are unchanged; concurrent callers share
+        launches.  Verify and ReconstructAndVerify stay unbatched."""
         _check(self._lib.blbrs_encoder_set_batcher(self._h, batcher._h if batcher else None))
         self._batcher = batcher  # keep it alive while attached
 
@@ -400,10 +401,11 @@ class Encoder:
 
 
 class Batcher:
-    """Batching queue for concurrent host Reconstruct / ReconstructData calls (SURVEY.md §8f
-    row 4; client/blb/reconstruct.go:65-195 with MaxInFlight > 1).  Calls that arrive
-    within `window_us` of the first waiting one (or until `max_batch` wait) run as one
-    kernel launch per (shape, erasure pattern, length) group.  Attach with
+    """Batching queue for concurrent host Encode / Reconstruct / ReconstructData calls
+    (client/blb/reconstruct.go:65-195 with MaxInFlight > 1, and
+    the tractserver's concurrent RSEncode RPCs, store.go:1099).  Calls that arrive within
+    `window_us` of the first waiting one (or until `max_batch` wait) run as one kernel launch
+    per (shape, plan, length) group.  Attach with
     Encoder.SetBatcher; free only after detaching from every encoder."""
 
     def __init__(self, max_batch: int = 64, window_us: int = 200, devices: Optional[Sequence[int]] = None):

@@ -87,11 +87,12 @@ func mapErr(rc C.int) error {
 	}
 }
 
-// EnableBatching makes every encoder created afterwards route its Reconstruct /
+// EnableBatching makes every encoder created afterwards route its Encode / Reconstruct /
 // ReconstructData calls through one process-wide batcher over all visible GPUs (blb_rs.h:
 // blbrs_batcher_new): concurrent degraded reads (client/blb/reconstruct.go with
-// ReconstructBehavior.MaxInFlight > 1) then share kernel launches.  Call once at client
-// start-up, before reads begin.
+// ReconstructBehavior.MaxInFlight > 1) and the increments of concurrent RSEncode RPCs
+// (internal/tractserver/store.go:1099) then share kernel launches.  Verify is never batched.
+// Call once at process start-up, before coding begins.
 func EnableBatching(maxBatch, windowMicros int) error {
 	var b *C.blbrs_batcher
 	if err := call(func() C.int { return C.blbrs_batcher_new(C.int(maxBatch), C.int(windowMicros), &b) }); err != nil {

@@ -260,15 +260,19 @@ int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_s
                             size_t stripe_stride, size_t batch, size_t shard_len, size_t block,
                             size_t phase, const uint32_t* seeds_dev, uint32_t* crc_out_dev, void* stream);
 
-/* ---- batched client reconstructs ----
+/* ---- batched host calls: client reconstructs and tractserver encodes (SURVEY.md §8f rows
+ * 4 and 1) ----
  * client/blb/reconstruct.go:65-195 calls ReconstructData once per degraded read (one stripe
- * of `length`-byte pieces), up to MaxInFlight (:19,35-45) at once.  A batcher collects
- * concurrent host Reconstruct / ReconstructData calls that arrive within window_us (or
- * until max_batch wait) and runs them as one kernel launch per (encoder, erasure pattern,
- * length) group plus one stream sync.  Attach it to an encoder and the plain
- * blbrs_reconstruct / blbrs_reconstruct_data calls on that encoder go through it: same
- * arguments, results and errors, the caller still blocks until its own stripe is done --
- * the Go Encoder interface is unchanged.  (blbrs_reconstruct_verify is never batched.)
+ * of `length`-byte pieces), up to MaxInFlight (:19,35-45) at once; the tractserver calls
+ * Encode once per 4 MiB increment of each RSEncode RPC (store.go:1099), up to
+ * RejectCtlReqThreshold = 1000 RPCs at once (internal/tractserver/config.go:91).  A batcher
+ * collects concurrent host Encode / Reconstruct / ReconstructData calls that arrive within
+ * window_us (or until max_batch wait) and runs them as one kernel launch per (encoder shape,
+ * plan, length) group plus one stream sync.  Attach it to an encoder and the plain
+ * blbrs_encode / blbrs_reconstruct / blbrs_reconstruct_data calls on that encoder go through
+ * it: same arguments, results and errors, the caller still blocks until its own stripe is
+ * done -- the Go Encoder interface is unchanged.  (blbrs_verify and blbrs_reconstruct_verify
+ * are never batched.)  A lone caller waits up to window_us longer per call.
  * Pinned / device shards are used in place; pageable ones are staged by the calling thread
  * through the pinned buffer pool.  Each device of the batcher has a queue drained by two
  * lanes (own stream each), so one batch is collected while the previous one runs.  A call

@@ -108,3 +108,52 @@ def test_batched_large_and_reconstruct_verify_not_batched():
     assert b.stats() == (1, 1)
     enc.SetBatcher(None)
     b.close()
+
+
+def test_batched_concurrent_encodes_match_oracle():
+    """The tractserver side: concurrent RSEncode RPCs each Encode one increment per call
+    (internal/tractserver/store.go:1099).  With a Batcher attached, Encode calls from many
+    threads share launches; parity (written over stale pool bytes) equals the oracle's."""
+    torch = _torch()
+    k, m = 6, 3
+    rng = np.random.default_rng(7)
+    sizes = [4096, 65536, (1 << 20) + 13]
+    data = {s: [rng.integers(0, 256, s, dtype=np.uint8) for _ in range(k)] for s in sizes}
+    want = {s: N.encode(k, m, data[s]) for s in sizes}
+    b = reedsolomon.Batcher(max_batch=32, window_us=2000)
+    enc = reedsolomon.New(k, m)
+    enc.SetBatcher(b)
+    errors = []
+
+    def server(tid):
+        for it in range(6):
+            size = sizes[(tid + it) % len(sizes)]
+            pinned = (tid + it) % 2 == 0
+            mk = (lambda a: torch.from_numpy(a).pin_memory().numpy()) if pinned else (lambda a: a.copy())
+            shards = [mk(x) for x in data[size]] + [mk(np.full(size, 0xEE, np.uint8)) for _ in range(m)]
+            try:
+                enc.Encode(shards)
+                for j in range(m):
+                    assert np.array_equal(shards[k + j], want[size][j]), (tid, it, j)
+                for i in range(k):
+                    assert np.array_equal(shards[i], data[size][i]), (tid, it, i)
+            except Exception as e:  # noqa: BLE001 -- collected and re-raised on the main thread
+                errors.append(e)
+
+    ths = [threading.Thread(target=server, args=(t,)) for t in range(16)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors[:3]
+    reqs, launches = b.stats()
+    assert reqs == 16 * 6
+    assert launches < reqs, (reqs, launches)
+    # Errors keep their types on the batched path; Verify is never batched.
+    with pytest.raises(reedsolomon.ErrShardSize):
+        enc.Encode([data[4096][0][:4095]] + [x.copy() for x in data[4096][1:]] + [np.zeros(4096, np.uint8)] * m)
+    ok_shards = [x.copy() for x in data[4096]] + [x.copy() for x in want[4096]]
+    assert enc.Verify(ok_shards)
+    assert b.stats()[0] == reqs
+    enc.SetBatcher(None)
+    b.close()

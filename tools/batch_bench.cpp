@@ -1,8 +1,12 @@
-// Client degraded-read throughput through the C ABI, with and without the reconstruct
-// batcher.  T threads x R calls of ReconstructData on RS(6,3)
-// stripes of L-byte pinned pieces, one missing data shard, a fresh encoder per call
-// (client/blb/reconstruct.go:172).  No Python in the loop.
-//   build: see tools/Makefile (target batch_bench); run: tools/_build/batch_bench [T] [R]
+// Host-call throughput through the C ABI, with and without the batcher.
+//   reconstruct (default): client degraded reads -- T threads x R calls
+//     of ReconstructData on RS(6,3) stripes of L-byte pinned pieces, one missing data shard, a
+//     fresh encoder per call (client/blb/reconstruct.go:172);
+//   encode: concurrent RSEncode RPCs (§8f row 1) -- T threads x R calls of Encode on RS(6,3)
+//     stripes of L-byte pinned increments (store.go:1099; EncodeIncrementSize 4 MiB, 1 MiB in
+//     tests), one encoder per RPC.
+// No Python in the loop.
+//   build: see tools/Makefile (target batch_bench); run: tools/_build/batch_bench [T] [R] [encode]
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -25,6 +29,7 @@ static void check(int rc, const char* what) {
 int main(int argc, char** argv) {
     const int T = argc > 1 ? std::atoi(argv[1]) : 64;
     const int R = argc > 2 ? std::atoi(argv[2]) : 50;
+    const bool encode = argc > 3 && std::strcmp(argv[3], "encode") == 0;
     const int k = 6, m = 3, n = k + m;
     {  // cost of the per-shard pointer classification under T-way contention
         uint8_t* p = nullptr;
@@ -43,7 +48,10 @@ int main(int argc, char** argv) {
                     T * static_cast<double>(N) / el);
         (void)hipHostFree(p);
     }
-    for (size_t L : {size_t{4} << 10, size_t{16} << 10, size_t{64} << 10, size_t{256} << 10, size_t{1} << 20}) {
+    const std::vector<size_t> lengths =
+        encode ? std::vector<size_t>{size_t{64} << 10, size_t{256} << 10, size_t{1} << 20, size_t{4} << 20}
+               : std::vector<size_t>{size_t{4} << 10, size_t{16} << 10, size_t{64} << 10, size_t{256} << 10, size_t{1} << 20};
+    for (size_t L : lengths) {
         // Per-thread pinned stripe + output.
         std::vector<uint8_t*> bufs(static_cast<size_t>(T) * (n + 1));
         for (auto& p : bufs) {
@@ -62,9 +70,13 @@ int main(int argc, char** argv) {
                         std::vector<uint8_t*> sh(n);
                         std::vector<size_t> lens(n, L);
                         for (int i = 0; i < n; ++i) sh[i] = bufs[static_cast<size_t>(t) * (n + 1) + i];
-                        sh[1] = bufs[static_cast<size_t>(t) * (n + 1) + n];  // output
-                        lens[1] = 0;
-                        check(blbrs_reconstruct_data(enc, sh.data(), lens.data()), "reconstruct_data");
+                        if (encode) {
+                            check(blbrs_encode(enc, sh.data(), lens.data()), "encode");
+                        } else {
+                            sh[1] = bufs[static_cast<size_t>(t) * (n + 1) + n];  // output
+                            lens[1] = 0;
+                            check(blbrs_reconstruct_data(enc, sh.data(), lens.data()), "reconstruct_data");
+                        }
                         blbrs_free(enc);
                     }
                 };
@@ -83,10 +95,11 @@ int main(int argc, char** argv) {
                 uint64_t r1 = 0, l1 = 0;
                 if (b) check(blbrs_batcher_stats(b, &r1, &l1), "stats");
                 const double calls = static_cast<double>(T) * R;
-                std::printf("{\"piece_bytes\": %zu, \"mode\": \"%s\", \"window_us\": %d, \"threads\": %d, \"calls\": %.0f, "
-                            "\"calls_per_s\": %.0f, \"GiBps_survivors_read\": %.3f, \"us_per_call_latency\": %.1f, "
+                std::printf("{\"op\": \"%s\", \"piece_bytes\": %zu, \"mode\": \"%s\", \"window_us\": %d, \"threads\": %d, "
+                            "\"calls\": %.0f, \"calls_per_s\": %.0f, \"GiBps_data_read\": %.3f, \"us_per_call_latency\": %.1f, "
                             "\"calls_per_launch\": %.2f}\n",
-                            L, batched ? "batched" : "per_call", window_us, T, calls, calls / el,
+                            encode ? "encode" : "reconstruct_data", L, batched ? "batched" : "per_call", window_us, T, calls,
+                            calls / el,
                             calls * k * L / el / (1u << 30), el * 1e6 / R,
                             b ? static_cast<double>(r1 - r0) / static_cast<double>(l1 - l0 ? l1 - l0 : 1) : 1.0);
                 std::fflush(stdout);

@@ -7,8 +7,9 @@
   * per-call Encode / ReconstructData on shards from the pinned buffer pool
     (blbrs_buffer_get = rpc.GetBuffer, pkg/rpc/pool.go) from 1..16 concurrent threads, the
     way concurrent RSEncode RPCs (internal/tractserver/store.go:1099) and degraded reads
-    (client/blb/reconstruct.go:173) call it.
-Prints one JSON object."""
+    (client/blb/reconstruct.go:173) call it, with and without a Batcher attached (concurrent
+    calls share launches).
+Prints one JSON object.  `--pool-only` runs just the pool-call sections."""
 from __future__ import annotations
 
 import json
@@ -41,6 +42,11 @@ def timeit(fn, reps):
 def main():
     dev = torch.device("cuda:0")
     out = {}
+    if "--pool-only" in sys.argv:
+        out["pool_calls"] = pool_calls(6, 3)
+        out["pool_calls_batched"] = pool_calls(6, 3, window_us=50)
+        print(json.dumps(out))
+        return
     n = 512 * MIB
     h = torch.empty(n, dtype=torch.uint8).pin_memory()
     h2 = torch.empty(n, dtype=torch.uint8).pin_memory()
@@ -103,16 +109,23 @@ def main():
                                                    "cpu_oracle_avx2_GiBps": round(cpu, 2),
                                                    "cpu_threads": threads}
     out["pool_calls"] = pool_calls(k, m)
+    out["pool_calls_batched"] = pool_calls(k, m, window_us=50)
     print(json.dumps(out))
 
 
-def pool_calls(k, m):
+def pool_calls(k, m, window_us=None):
     """Per-call host Encode / ReconstructData of one stripe of 4 MiB pool buffers per call,
-    T threads each looping over its own stripe for ~2 s."""
+    T threads each looping over its own stripe for ~2 s; with `window_us`, through a Batcher
+    (max_batch 32) attached to the encoder."""
     res = {}
     S = 4 * MIB
     enc = rs.New(k, m, devices=[0])
-    for T in (1, 2, 4, 8, 16):
+    batcher = None
+    if window_us is not None:
+        batcher = rs.Batcher(max_batch=32, window_us=window_us, devices=[0])
+        enc.SetBatcher(batcher)
+        res["window_us"] = window_us
+    for T in ((1, 2, 4, 8, 16) if batcher is None else (1, 4, 8, 16, 32)):
         stripes = []
         for t in range(T):
             sh = [rs.GetBuffer(S) for _ in range(k + m)]
@@ -151,6 +164,10 @@ def pool_calls(k, m):
                 rs.PutBuffer(b)
     res["shard_bytes"] = S
     res["device_stats"] = rs.device_stats(0)
+    if batcher is not None:
+        res["batcher_requests"], res["batcher_launches"] = batcher.stats()
+        enc.SetBatcher(None)
+        batcher.close()
     return res
 
 
