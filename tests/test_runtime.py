@@ -270,8 +270,8 @@ def test_pool_buffers_code_zero_copy(oracle_lib):
 
 @pytest.mark.gpu
 def test_batcher_on_device_list():
-    """A batcher created on an explicit device list serves a host ReconstructData call in
-    one launch (its lanes live on the listed device)."""
+    """A batcher created on an explicit device list serves a host Encode and a host
+    ReconstructData call, one launch each (its lanes live on the listed device)."""
     import torch
     k, m, S = 4, 2, 4096
     b = rs.Batcher(max_batch=8, window_us=100, devices=[0])
@@ -287,7 +287,7 @@ def test_batcher_on_device_list():
         enc.ReconstructData(sh)
         assert np.array_equal(sh[0], ref)
         r, launches = b.stats()
-        assert r == 1 and launches == 1
+        assert r == 2 and launches == 2
         enc.SetBatcher(None)
     finally:
         b.close()
