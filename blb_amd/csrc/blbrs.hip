@@ -21,6 +21,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -522,6 +523,11 @@ struct BatchReq {
     std::chrono::steady_clock::time_point arrival;
     int rc = BLBRS_OK;
     std::string msg;              // error text, re-raised on the caller's thread
+    // Completion: per request, so a finished batch wakes only its own callers (a shared
+    // condition variable woke every waiting caller on every batch and serialised them on the
+    // queue mutex: 64 callers of 64 KiB pieces ran at 77k calls/s against 96k per call).
+    std::mutex m;
+    std::condition_variable cv;
     bool done = false;
 };
 
@@ -544,7 +550,6 @@ struct blbrs_batcher {
     std::chrono::microseconds window{200};
     std::vector<int> devices;  // distinct devices
     std::mutex mu;
-    std::condition_variable cv_done;
     std::map<int, Queue> queues;
     std::vector<std::unique_ptr<Lane>> lanes;
     std::atomic<unsigned> rr{0};
@@ -570,9 +575,14 @@ struct blbrs_batcher {
             if (!qu.q.empty()) qu.cv.notify_one();
             lk.unlock();
             process(lane, batch);
+            for (BatchReq* r : batch) {
+                // Notify under the request's lock: once it is released the caller may return
+                // and destroy the request.
+                std::lock_guard<std::mutex> g(r->m);
+                r->done = true;
+                r->cv.notify_one();
+            }
             lk.lock();
-            for (BatchReq* r : batch) r->done = true;
-            cv_done.notify_all();
         }
     }
 
@@ -721,10 +731,13 @@ int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key,
     }
     req.arrival = std::chrono::steady_clock::now();
     {
-        std::unique_lock<std::mutex> lk(b->mu);
+        std::lock_guard<std::mutex> lk(b->mu);
         if (b->stop) return fail(BLBRS_ERR_INVALID_ARG, "batcher is shutting down");
         b->enqueue(&req);
-        b->cv_done.wait(lk, [&] { return req.done; });
+    }
+    {
+        std::unique_lock<std::mutex> lk(req.m);
+        req.cv.wait(lk, [&] { return req.done; });
     }
     if (req.rc != BLBRS_OK) return fail(req.rc, req.msg);
     for (int32_t i : hp->out_idx)
@@ -739,9 +752,13 @@ int make_batcher(int max_batch, int window_us, std::vector<int> devs, blbrs_batc
     b->max_batch = static_cast<size_t>(max_batch);
     b->window = std::chrono::microseconds(window_us);
     b->devices = devs;
+    // Launch lanes per device queue (default 2: one batch collects while the previous runs);
+    // $BLBRS_BATCH_LANES = 1..8 overrides it (tuning).
+    int nlanes = 2;
+    if (const char* env = std::getenv("BLBRS_BATCH_LANES"); env && *env) nlanes = std::min(8, std::max(1, std::atoi(env)));
     for (int d : devs) {
         b->queues[d];
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < nlanes; ++j) {
             auto lane = std::make_unique<blbrs_batcher::Lane>();
             lane->device = d;
             rt::DeviceGuard guard;

@@ -405,10 +405,12 @@ class Batcher:
     (client/blb/reconstruct.go:65-195 with MaxInFlight > 1, and
     the tractserver's concurrent RSEncode RPCs, store.go:1099).  Calls that arrive within
     `window_us` of the first waiting one (or until `max_batch` wait) run as one kernel launch
-    per (shape, plan, length) group.  Attach with
+    per (shape, plan, length) group.  window_us = 0 (default) batches naturally: a free lane
+    takes whatever is queued at once, and calls that arrive while the lanes are busy form
+    the next batch, so a lone caller waits for nothing.  Attach with
     Encoder.SetBatcher; free only after detaching from every encoder."""
 
-    def __init__(self, max_batch: int = 64, window_us: int = 200, devices: Optional[Sequence[int]] = None):
+    def __init__(self, max_batch: int = 64, window_us: int = 0, devices: Optional[Sequence[int]] = None):
         self._lib = _lib.load()
         h = ctypes.c_void_p()
         if devices is None:

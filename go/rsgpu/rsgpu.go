@@ -92,7 +92,8 @@ func mapErr(rc C.int) error {
 // blbrs_batcher_new): concurrent degraded reads (client/blb/reconstruct.go with
 // ReconstructBehavior.MaxInFlight > 1) and the increments of concurrent RSEncode RPCs
 // (internal/tractserver/store.go:1099) then share kernel launches.  Verify is never batched.
-// Call once at process start-up, before coding begins.
+// Call once at process start-up, before coding begins; windowMicros = 0 batches naturally
+// (no added wait for a lone caller).
 func EnableBatching(maxBatch, windowMicros int) error {
 	var b *C.blbrs_batcher
 	if err := call(func() C.int { return C.blbrs_batcher_new(C.int(maxBatch), C.int(windowMicros), &b) }); err != nil {

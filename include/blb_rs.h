@@ -272,7 +272,10 @@ int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_s
  * blbrs_encode / blbrs_reconstruct / blbrs_reconstruct_data calls on that encoder go through
  * it: same arguments, results and errors, the caller still blocks until its own stripe is
  * done -- the Go Encoder interface is unchanged.  (blbrs_verify and blbrs_reconstruct_verify
- * are never batched.)  A lone caller waits up to window_us longer per call.
+ * are never batched.)  window_us = 0 batches naturally: a free lane takes whatever is
+ * queued at once and calls arriving while the lanes are busy form the next batch, so a lone
+ * caller does not wait; a positive window holds a batch open up to window_us after its first
+ * call.
  * Pinned / device shards are used in place; pageable ones are staged by the calling thread
  * through the pinned buffer pool.  Each device of the batcher has a queue drained by two
  * lanes (own stream each), so one batch is collected while the previous one runs.  A call

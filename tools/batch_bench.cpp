@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
             for (size_t i = 0; i < L; ++i) p[i] = static_cast<uint8_t>(std::rand());
         }
         for (int batched = 0; batched < 2; ++batched) {
-            for (int window_us : batched ? std::vector<int>{50, 200} : std::vector<int>{0}) {
+            for (int window_us : batched ? std::vector<int>{0, 50, 200} : std::vector<int>{0}) {
                 blbrs_batcher* b = nullptr;
                 if (batched) check(blbrs_batcher_new(T, window_us, &b), "batcher_new");
                 auto client = [&](int t, int reps) {
