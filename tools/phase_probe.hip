@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1); } } while (0)
@@ -83,6 +84,33 @@ __global__ __launch_bounds__(256) void policy_kernel(uint8_t* base, uint32_t B) 
         st_pol<SP>(s + 6 * S + u * kStep, a ^ c);
         st_pol<SP>(s + 7 * S + u * kStep, a);
         st_pol<SP>(s + 8 * S + u * kStep, c);
+    }
+}
+
+// One tile per block of NTH threads (U 16-byte chunks per lane per shard): tile = NTH*16*U
+// bytes per shard, XCD-contiguous.  Does a larger contiguous tile per block (fewer,
+// longer concurrent streams) raise the read-6/write-3 ceiling?
+template <int NTH, int U>
+__global__ __launch_bounds__(NTH) void wide_kernel(uint8_t* base, uint32_t B) {
+    constexpr uint32_t step = NTH * 16;
+    const uint32_t tps = S / (step * U);
+    const uint32_t total = B * tps;
+    const uint32_t t = (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u;
+    if (t >= total) return;
+    const uint32_t b = t / tps;
+    uint8_t* s = base + b * 9 * S + static_cast<uint64_t>(t - b * tps) * step * U + threadIdx.x * 16;
+    u32x4 x[6][U];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[r][u] = ld(s + r * S + u * step);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const u32x4 a = x[0][u] ^ x[1][u] ^ x[2][u];
+        const u32x4 c = x[3][u] ^ x[4][u] ^ x[5][u];
+        st(s + 6 * S + u * step, a ^ c);
+        st(s + 7 * S + u * step, a);
+        st(s + 8 * S + u * step, c);
     }
 }
 
@@ -158,6 +186,18 @@ int main(int argc, char** argv) {
 
     auto report = [&](const char* tag, double ms) { printf("%-48s %8.3f ms %8.1f GB/s\n", tag, ms, alg / ms / 1e6); fflush(stdout); };
     char tag[128];
+    if (argc > 2 && std::string(argv[2]) == "wide") {  // phase_probe B wide: tile-size sweep
+        for (int rep = 0; rep < 3; ++rep) {
+            printf("# wide rep %d\n", rep);
+#define WIDE(NTH, U, LDS) { const uint32_t g = (B * (S / (NTH * 16u * U)) + 7) & ~7u; \
+            snprintf(tag, sizeof tag, "wide threads=%4d U=%d tile=%3u KiB lds=%3u KiB", NTH, U, NTH * 16 * U / 1024, LDS); \
+            report(tag, time_ms([&] { hipLaunchKernelGGL((wide_kernel<NTH, U>), dim3(g), dim3(NTH), LDS * 1024, 0, base, B); })); }
+            WIDE(256, 4, 0) WIDE(256, 4, 96) WIDE(512, 4, 0) WIDE(512, 2, 0) WIDE(1024, 2, 0) WIDE(1024, 1, 0) WIDE(256, 8, 0) WIDE(512, 4, 96)
+#undef WIDE
+        }
+        CK(hipFree(base));
+        return 0;
+    }
     if (argc > 2) {  // phase_probe B policy: store cache-policy A/B on the encode's pattern
         const uint32_t g4 = (B * (S / (kStep * 4)) + 7) & ~7u;
         for (int rep = 0; rep < 3; ++rep) {

@@ -188,10 +188,11 @@ static void stride_probe(CodeArgs a) {
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "zc") { zero_copy_probe(); return 0; }
     const bool ntab = argc > 1 && std::string(argv[1]) == "nt";
+    const bool occ = argc > 1 && std::string(argv[1]) == "occ";
     const bool stride = argc > 1 && std::string(argv[1]) == "stride";
     const bool pmc = argc > 1 && std::string(argv[1]) == "pmc";
     const bool ceil = argc > 1 && std::string(argv[1]) == "ceil";
-    if (argc > 1 && !pmc && !stride && !ceil && !ntab) B = static_cast<uint32_t>(atoi(argv[1]));
+    if (argc > 1 && !pmc && !stride && !ceil && !ntab && !occ) B = static_cast<uint32_t>(atoi(argv[1]));
     const size_t total = size_t(B) * 9 * S;
     CK(hipMalloc(&g_base, total));
     CK(hipMalloc(&g_sink, 64));
@@ -242,6 +243,25 @@ int main(int argc, char** argv) {
         CK(hipDeviceSynchronize());
         printf("pmc launches done: read_bytes=%.0f copy_bytes=%.0f+%.0f rs63_bytes=%.0f+%.0f\n", double(B) * 9 * S,
                double(B) * S, double(B) * S, double(B) * 6 * S, double(B) * 3 * S);
+        return 0;
+    }
+    if (occ) {
+        // Occupancy of the shipped encode grid, capped by an unused dynamic LDS allocation:
+        // 0 = natural (VGPR-limited), 56 KiB = at most 2 blocks per CU, 96 KiB = 1 block per CU.
+        CodeArgs c = a;
+        c.tiles_per_stripe = static_cast<uint32_t>(S / 16384);
+        c.xcd_remap = 1;
+        const int grid = static_cast<int>(c.B * c.tiles_per_stripe) & ~7;
+        const double bytes = double(c.B) * 9 * S;
+        for (int rep = 0; rep < 3; ++rep)
+            for (unsigned lds : {0u, 56u << 10, 96u << 10}) {
+                double ms = time_ms([&] { hipLaunchKernelGGL((rs_code_kernel<6, 3, 0, 0, 4, 3>), dim3(grid), dim3(256), lds, 0, c); });
+                printf("occ rep %d rs63 U=4 dyn_lds=%6u : %8.3f ms  %7.1f GB/s\n", rep, lds, ms, bytes / ms / 1e6);
+                const uint32_t tps4 = static_cast<uint32_t>(S / 16384);
+                ms = time_ms([&] { hipLaunchKernelGGL((pattern_kernel<6, 3, 4, 3, 1>), dim3(grid), dim3(256), lds, 0, g_base, S, 9 * S, B, tps4, g_sink); });
+                printf("occ rep %d pattern R6W3 U=4 dyn_lds=%6u : %8.3f ms  %7.1f GB/s\n", rep, lds, ms, bytes / ms / 1e6);
+                fflush(stdout);
+            }
         return 0;
     }
     if (ntab) {
