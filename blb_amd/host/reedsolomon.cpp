@@ -1,6 +1,7 @@
 // reedsolomon.cpp -- the Encoder mirror over include/blb_rs.h (see reedsolomon.hpp).
 #include "reedsolomon.hpp"
 
+#include <atomic>
 #include <vector>
 
 #include "../../include/blb_rs.h"
@@ -47,10 +48,35 @@ const char* ErrString(Err e) {
 
 std::string Encoder::LastEngineError() { return blbrs_last_error(); }
 
+namespace {
+std::atomic<blbrs_batcher*> g_batcher{nullptr};
+}
+
+Err EnableBatching(int maxBatch, int windowMicros) {
+    blbrs_batcher* b = nullptr;
+    const int rc = blbrs_batcher_new(maxBatch, windowMicros, &b);
+    if (rc != BLBRS_OK) return map_rc(rc);
+    blbrs_batcher* none = nullptr;
+    if (!g_batcher.compare_exchange_strong(none, b)) {  // already on: keep the first
+        blbrs_batcher_free(b);
+    }
+    return Err::None;
+}
+
+void DisableBatching() {
+    if (blbrs_batcher* b = g_batcher.exchange(nullptr)) blbrs_batcher_free(b);
+}
+
+void BatchingStats(uint64_t* requests, uint64_t* launches) {
+    *requests = *launches = 0;
+    if (blbrs_batcher* b = g_batcher.load()) blbrs_batcher_stats(b, requests, launches);
+}
+
 std::pair<std::unique_ptr<Encoder>, Err> New(int dataShards, int parityShards) {
     blbrs_encoder* h = nullptr;
     const int rc = blbrs_new(dataShards, parityShards, &h);
     if (rc != BLBRS_OK) return {nullptr, map_rc(rc)};
+    if (blbrs_batcher* b = g_batcher.load()) blbrs_encoder_set_batcher(h, b);
     return {std::unique_ptr<Encoder>(new Encoder(h, dataShards, parityShards)), Err::None};
 }
 

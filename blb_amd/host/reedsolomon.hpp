@@ -11,6 +11,7 @@
 // shards is a std::vector<blb::Bytes> (Go [][]byte): len 0 = missing; a missing shard with
 // cap >= size is resliced in place, otherwise a new buffer is made -- exactly klauspost.
 #pragma once
+#include <cstdint>
 #include <memory>
 #include <string>
 #include <utility>
@@ -67,5 +68,15 @@ class Encoder {
 
 // reedsolomon.New(dataShards, parityShards)
 std::pair<std::unique_ptr<Encoder>, Err> New(int dataShards, int parityShards);
+
+// Extension (the Go shim's rsgpu.EnableBatching): every encoder New returns afterwards routes
+// its Encode / Reconstruct / ReconstructData through one process-wide batcher
+// (blbrs_batcher_new), so concurrent RSEncode RPCs and degraded reads share kernel
+// launches.  windowMicros = 0 batches naturally.  DisableBatching frees it: call it only once
+// every encoder made while batching was on has been destroyed.
+Err EnableBatching(int maxBatch, int windowMicros);
+void DisableBatching();
+// Calls served and kernel launches issued by the batcher so far (0, 0 when off).
+void BatchingStats(uint64_t* requests, uint64_t* launches);
 
 }  // namespace reedsolomon

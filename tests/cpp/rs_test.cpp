@@ -592,6 +592,54 @@ static void TestPackThenRSEncode(T* t) {
     if (verr2 != reedsolomon::Err::None || ok2) t->Errorf("corrupted parity verified");
 }
 
+// The tractserver under load: concurrent RSEncode RPCs (internal/tractserver/server.go:553-582,
+// up to RejectCtlReqThreshold at once) with batching on (reedsolomon::EnableBatching, the Go
+// shim's rsgpu.EnableBatching).  Every RPC's parity must verify, and the increments of
+// different RPCs must have shared launches.
+static void TestRSEncodeConcurrentBatched(T* t) {
+    const int N = 6, M = 3, B = 200000, inc = 65536, R = 12;
+    if (reedsolomon::EnableBatching(64, 0) != reedsolomon::Err::None) Fatalf("EnableBatching failed");
+    std::vector<std::vector<Bytes>> data(R);
+    std::vector<std::unique_ptr<memTractserverTalker>> talkers;
+    std::vector<std::vector<core::TSAddr>> addrs(R);
+    for (int r = 0; r < R; ++r) {
+        talkers.push_back(std::make_unique<memTractserverTalker>());
+        addrs[r] = makeAddrs(N + M);
+        std::mt19937_64 rng(97531 * (r + 1));
+        data[r].resize(N + M);
+        for (int i = 0; i < N; ++i) data[r][i] = randBytes(rng, B);
+        for (int64_t off = 0; off < B; off += inc) {
+            const int64_t end = std::min<int64_t>(off + inc, B);
+            for (int i = 0; i < N; ++i)
+                talkers[r]->addCtlReadReply(addrs[r][i].Host, data[r][i].slice(off, end), Error::ErrEOF);
+            for (int i = N; i < N + M; ++i) talkers[r]->addCtlWriteReply(addrs[r][i].Host, Error::NoError);
+        }
+    }
+    std::vector<Error> errs(R, Error::NoError);
+    std::vector<std::thread> th;
+    for (int r = 0; r < R; ++r)
+        th.emplace_back([&, r] {
+            tractserver::Store s(talkers[r].get(), tractserver::Config{inc, r % 2 == 1});
+            std::vector<core::TSAddr> srcs(addrs[r].begin(), addrs[r].begin() + N), dests(addrs[r].begin() + N, addrs[r].end());
+            errs[r] = s.RSEncode(cid, B, srcs, dests, {});
+        });
+    for (auto& x : th) x.join();
+    uint64_t requests = 0, launches = 0;
+    reedsolomon::BatchingStats(&requests, &launches);
+    reedsolomon::DisableBatching();  // every RPC's encoder is gone
+    auto [enc, e] = reedsolomon::New(N, M);
+    for (int r = 0; r < R; ++r) {
+        if (errs[r] != Error::NoError) t->Errorf("RPC %d: %s", r, core::String(errs[r]));
+        for (int i = N; i < N + M; ++i)
+            for (const auto& w : talkers[r]->ctlWriteCalls[addrs[r][i].Host]) data[r][i] = concat(data[r][i], w.B);
+        auto [ok, verr] = enc->Verify(data[r]);
+        if (verr != reedsolomon::Err::None || !ok) t->Errorf("RPC %d: parity does not verify", r);
+    }
+    const uint64_t calls = static_cast<uint64_t>(R) * ((B + inc - 1) / inc);
+    if (requests != calls) t->Errorf("batcher served %llu calls, want %llu", (unsigned long long)requests, (unsigned long long)calls);
+    if (launches >= requests) t->Errorf("no launch was shared (%llu launches)", (unsigned long long)launches);
+}
+
 int main(int argc, char** argv) {
     const bool cpu_only = argc > 1 && std::string(argv[1]) == "--cpu";
     struct Test { const char* name; void (*fn)(T*); bool gpu; };
@@ -614,6 +662,7 @@ int main(int argc, char** argv) {
         {"TestRSEncodeStopsAtFailingRead/pipelined", [](T* t) { TestRSEncodeStopsAtFailingRead(t, true); }, true},
         {"TestRSEncodeStopsAtFailingWrite", [](T* t) { TestRSEncodeStopsAtFailingWrite(t, false); }, true},
         {"TestRSEncodeStopsAtFailingWrite/pipelined", [](T* t) { TestRSEncodeStopsAtFailingWrite(t, true); }, true},
+        {"TestRSEncodeConcurrentBatched", TestRSEncodeConcurrentBatched, true},
     };
     int failed = 0, ran = 0;
     for (const Test& tc : tests) {
