@@ -515,8 +515,10 @@ std::vector<uint8_t> present_vec(const blbrs_encoder* enc, const uint8_t* presen
 // place; pageable shards are staged by the CALLING thread through a pooled pinned buffer.
 struct BatchReq {
     EncoderCore* core = nullptr;
-    std::shared_ptr<HostPlan> hp;
-    std::string key;
+    std::shared_ptr<HostPlan> hp;   // store step (encode / decode plan); null = verify only
+    std::shared_ptr<HostPlan> vp;   // verify step after it (the encode plan); null = none
+    std::string key;                // group key: plan key, "+V" when verifying
+    int ok = 0;                     // verify result (vp set)
     std::vector<uint64_t> views;  // device-visible address per shard slot (0 = unused)
     size_t S = 0;
     int dev = -1;                 // device that must run it (device-memory shards), -1 = any
@@ -544,6 +546,9 @@ struct blbrs_batcher {
         uint64_t* tab_host = nullptr;
         uint64_t* tab_dev = nullptr;
         size_t tab_cap = 0;
+        int32_t* flags_host = nullptr;  // per-stripe Verify mismatch flags
+        int32_t* flags_dev = nullptr;
+        size_t flags_cap = 0;
         std::thread th;
     };
     size_t max_batch = 64;
@@ -609,9 +614,28 @@ struct blbrs_batcher {
         return BLBRS_OK;
     }
 
+    int flags(Lane* lane, size_t count) {
+        if (count > lane->flags_cap) {
+            if (lane->flags_host) (void)hipHostFree(lane->flags_host);
+            if (lane->flags_dev) (void)hipFree(lane->flags_dev);
+            lane->flags_host = nullptr;
+            lane->flags_dev = nullptr;
+            lane->flags_cap = 0;
+            const size_t cap = std::max<size_t>(count, 256);
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&lane->flags_host), cap * 4, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&lane->flags_dev), cap * 4));
+            lane->flags_cap = cap;
+        }
+        HIP_TRY(hipMemsetAsync(lane->flags_dev, 0, count * 4, lane->stream));
+        return BLBRS_OK;
+    }
+
     void process(Lane* lane, std::vector<BatchReq*>& batch) {
         // Handles of one (k, m) share a core, so calls from different encoders merge.  The
-        // groups share the lane's table, so they run one after the other.
+        // groups share the lane's table, so they run one after the other.  A group runs its
+        // store step (encode / decode) and then, for Verify / ReconstructAndVerify, the encode
+        // plan in verify mode over the same table: per-stripe mismatch flags come back with
+        // the one sync (store.go:1132-1142 in one round trip for the whole group).
         std::map<std::tuple<EncoderCore*, std::string, size_t>, std::vector<BatchReq*>> groups;
         for (BatchReq* r : batch) groups[{r->core, r->key, r->S}].push_back(r);
         rt::LoadTicket ticket;
@@ -619,8 +643,13 @@ struct blbrs_batcher {
         for (auto& [gk, reqs] : groups) {
             EncoderCore* core = std::get<0>(gk);
             const size_t S = std::get<2>(gk), n = static_cast<size_t>(core->k + core->m);
+            const BatchReq& r0 = *reqs[0];
+            const std::string plan_key_ = std::get<1>(gk).substr(0, std::get<1>(gk).size() - (r0.vp ? 2 : 0));
             const DevPlan* plan = nullptr;
-            int rc = core->dev_plan(std::get<1>(gk), *reqs[0]->hp, lane->device, &plan);
+            const DevPlan* vplan = nullptr;
+            int rc = BLBRS_OK;
+            if (r0.hp) rc = core->dev_plan(plan_key_, *r0.hp, lane->device, &plan);
+            if (rc == BLBRS_OK && r0.vp) rc = core->dev_plan("E", *r0.vp, lane->device, &vplan);
             if (rc == BLBRS_OK) {
                 std::vector<uint64_t> table(reqs.size() * n);
                 for (size_t j = 0; j < reqs.size(); ++j)
@@ -628,15 +657,28 @@ struct blbrs_batcher {
                 Stripes st;
                 st.nshards = static_cast<uint32_t>(n);
                 rc = upload(lane, table, &st.ptrs, &st.aligned);
-                if (rc == BLBRS_OK) rc = run_plan(*plan, st, reqs.size(), S, Mode::kStore, nullptr, lane->stream);
+                if (rc == BLBRS_OK && plan)
+                    rc = run_plan(*plan, st, reqs.size(), S, Mode::kStore, nullptr, lane->stream);
+                if (rc == BLBRS_OK && vplan) {
+                    rc = flags(lane, reqs.size());
+                    if (rc == BLBRS_OK)
+                        rc = run_plan(*vplan, st, reqs.size(), S, Mode::kVerify, lane->flags_dev, lane->stream);
+                    if (rc == BLBRS_OK) {
+                        const hipError_t e = hipMemcpyAsync(lane->flags_host, lane->flags_dev, reqs.size() * 4,
+                                                            hipMemcpyDeviceToHost, lane->stream);
+                        if (e != hipSuccess) rc = hip_fail(e, "batched verify flags");
+                    }
+                }
                 if (rc == BLBRS_OK) launches.fetch_add(1);
-                // The table is rewritten by the next group: wait for this one's launch.
+                // The table is rewritten by the next group: wait for this one's launches.
                 const hipError_t e = hipStreamSynchronize(lane->stream);
                 if (rc == BLBRS_OK && e != hipSuccess) rc = hip_fail(e, "batched call");
             }
-            for (BatchReq* r : reqs) {
+            for (size_t j = 0; j < reqs.size(); ++j) {
+                BatchReq* r = reqs[j];
                 r->rc = rc;
                 if (rc != BLBRS_OK) r->msg = rt::last_error();
+                else if (r->vp) r->ok = lane->flags_host[j] == 0;
             }
         }
         requests.fetch_add(batch.size());
@@ -676,6 +718,8 @@ struct blbrs_batcher {
             if (l->stream) (void)hipStreamDestroy(l->stream);
             if (l->tab_host) (void)hipHostFree(l->tab_host);
             if (l->tab_dev) (void)hipFree(l->tab_dev);
+            if (l->flags_host) (void)hipHostFree(l->flags_host);
+            if (l->flags_dev) (void)hipFree(l->flags_dev);
         }
     }
 };
@@ -685,24 +729,32 @@ namespace {
 // The host Encode / Reconstruct / ReconstructData of one stripe through `b` (blocking).  `hp`
 // is the encode or decode plan (at least one output), `key` its cache key; argument checks
 // have been done.
-int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key,
-                        std::shared_ptr<HostPlan> hp, uint8_t* const* shards, size_t S) {
+int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key, std::shared_ptr<HostPlan> hp,
+                 std::shared_ptr<HostPlan> vp, uint8_t* const* shards, size_t S, int* ok) {
     const int n = enc->k + enc->m;
     BatchReq req;
     req.core = enc->core.get();
     req.hp = hp;
-    req.key = key;
+    req.vp = vp;
+    req.key = vp ? key + "+V" : key;
     req.S = S;
     req.views.assign(n, 0);
-    // Slots touched by the plan: inputs then outputs; pageable ones get a staging slot.
-    std::vector<std::pair<int, bool>> touched;
-    for (int32_t i : hp->in_idx) touched.push_back({i, true});
-    for (int32_t i : hp->out_idx) touched.push_back({i, false});
+    // Slots the steps touch; the store step's outputs are written, every other slot is read.
+    // Pageable slots get a staging slot: read ones are copied in, written ones copied out.
+    std::vector<char> touched(n, 0), written(n, 0);
+    if (hp) {
+        for (int32_t i : hp->in_idx) touched[i] = 1;
+        for (int32_t i : hp->out_idx) touched[i] = written[i] = 1;
+    }
+    if (vp) {
+        for (int32_t i : vp->in_idx) touched[i] = 1;
+        for (int32_t i : vp->out_idx) touched[i] = 1;
+    }
     const size_t Sp = round_up(S, 256);
     size_t nstaged = 0;
     std::vector<int> slot(n, -1);
-    for (auto [i, in] : touched) {
-        (void)in;
+    for (int i = 0; i < n; ++i) {
+        if (!touched[i]) continue;
         int owner = -1;
         if (!rt::device_view(shards[i], &req.views[i], &owner)) {
             slot[i] = static_cast<int>(nstaged++);
@@ -722,10 +774,10 @@ int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key,
         size_t cap = 0;
         int rc = rt::pool_get(nstaged * Sp, &stage.p, &cap);
         if (rc) return rc;
-        for (auto [i, in] : touched) {
+        for (int i = 0; i < n; ++i) {
             if (slot[i] < 0) continue;
             uint8_t* p = stage.p + static_cast<size_t>(slot[i]) * Sp;
-            if (in) std::memcpy(p, shards[i], S);
+            if (!written[i]) std::memcpy(p, shards[i], S);
             if (!rt::device_view(p, &req.views[i])) return fail(BLBRS_ERR_HIP, "pinned staging has no device mapping");
         }
     }
@@ -740,8 +792,9 @@ int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key,
         req.cv.wait(lk, [&] { return req.done; });
     }
     if (req.rc != BLBRS_OK) return fail(req.rc, req.msg);
-    for (int32_t i : hp->out_idx)
-        if (slot[i] >= 0) std::memcpy(shards[i], stage.p + static_cast<size_t>(slot[i]) * Sp, S);
+    for (int i = 0; i < n; ++i)
+        if (written[i] && slot[i] >= 0) std::memcpy(shards[i], stage.p + static_cast<size_t>(slot[i]) * Sp, S);
+    if (ok) *ok = req.ok;
     return BLBRS_OK;
 }
 
@@ -866,7 +919,7 @@ int blbrs_encode(blbrs_encoder* enc, uint8_t* const* shards, const size_t* lens)
     for (int i = 0; i < n; ++i)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     auto hp = enc->encode_plan();
-    if (blbrs_batcher* b = enc->batcher.load()) return batched_call(b, enc, "E", hp, shards, S);
+    if (blbrs_batcher* b = enc->batcher.load()) return batched_call(b, enc, "E", hp, nullptr, shards, S, nullptr);
     return host_call(enc, {Step{"E", hp.get(), Mode::kStore}}, shards, S, nullptr);
 }
 
@@ -879,6 +932,8 @@ int blbrs_verify(blbrs_encoder* enc, const uint8_t* const* shards, const size_t*
     for (int i = 0; i < n; ++i)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     auto hp = enc->encode_plan();
+    if (blbrs_batcher* b = enc->batcher.load())
+        return batched_call(b, enc, "V", nullptr, hp, const_cast<uint8_t* const*>(shards), S, ok);
     return host_call(enc, {Step{"E", hp.get(), Mode::kVerify}}, const_cast<uint8_t* const*>(shards), S, ok);
 }
 
@@ -896,10 +951,12 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
         npresent += present[i];
     }
     auto ep = enc->encode_plan();
+    blbrs_batcher* b = enc->batcher.load();
     if (npresent == n) {  // nothing to rebuild; reconstructAndVerify still verifies
         if (!verify_ok) return BLBRS_OK;
         for (int i = 0; i < n; ++i)
             if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
+        if (b) return batched_call(b, enc, "V", nullptr, ep, shards, S, verify_ok);
         return host_call(enc, {Step{"E", ep.get(), Mode::kVerify}}, shards, S, verify_ok);
     }
     if (npresent < enc->k) return fail(BLBRS_ERR_TOO_FEW_SHARDS, "too few shards given");
@@ -909,9 +966,10 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     for (int32_t i : hp->out_idx)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "missing shard has no output buffer");
-    blbrs_batcher* b = verify_ok ? nullptr : enc->batcher.load();
     if (b && !hp->out_idx.empty()) {
-        if ((rc = batched_call(b, enc, plan_key(false, present, data_only), hp, shards, S))) return rc;
+        if ((rc = batched_call(b, enc, plan_key(false, present, data_only), hp, verify_ok ? ep : nullptr, shards, S,
+                               verify_ok)))
+            return rc;
         for (int32_t i : hp->out_idx) lens[i] = S;
         return BLBRS_OK;
     }

@@ -70,7 +70,7 @@ class Encoder {
 std::pair<std::unique_ptr<Encoder>, Err> New(int dataShards, int parityShards);
 
 // Extension (the Go shim's rsgpu.EnableBatching): every encoder New returns afterwards routes
-// its Encode / Reconstruct / ReconstructData through one process-wide batcher
+// its Encode / Verify / Reconstruct / ReconstructData through one process-wide batcher
 // (blbrs_batcher_new), so concurrent RSEncode RPCs and degraded reads share kernel
 // launches.  windowMicros = 0 batches naturally.  DisableBatching frees it: call it only once
 // every encoder made while batching was on has been destroyed.

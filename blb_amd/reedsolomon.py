@@ -133,9 +133,9 @@ class Encoder:
             self._h = None
 
     def SetBatcher(self, batcher: Optional["Batcher"]) -> None:
-        """Route this encoder's host Encode / Reconstruct / ReconstructData calls through
-        `batcher` (None detaches).  Results and errors are unchanged; concurrent callers share
-        launches.  Verify and ReconstructAndVerify stay unbatched."""
+        """Route this encoder's host Encode / Verify / Reconstruct / ReconstructData /
+        ReconstructAndVerify calls through `batcher` (None detaches).  Results and errors are
+        unchanged; concurrent callers share launches."""
         _check(self._lib.blbrs_encoder_set_batcher(self._h, batcher._h if batcher else None))
         self._batcher = batcher  # keep it alive while attached
 
@@ -401,7 +401,7 @@ class Encoder:
 
 
 class Batcher:
-    """Batching queue for concurrent host Encode / Reconstruct / ReconstructData calls
+    """Batching queue for concurrent host Encode / Verify / Reconstruct / ReconstructData calls
     (client/blb/reconstruct.go:65-195 with MaxInFlight > 1, and
     the tractserver's concurrent RSEncode RPCs, store.go:1099).  Calls that arrive within
     `window_us` of the first waiting one (or until `max_batch` wait) run as one kernel launch

@@ -87,11 +87,12 @@ func mapErr(rc C.int) error {
 	}
 }
 
-// EnableBatching makes every encoder created afterwards route its Encode / Reconstruct /
-// ReconstructData calls through one process-wide batcher over all visible GPUs (blb_rs.h:
+// EnableBatching makes every encoder created afterwards route its Encode / Verify /
+// Reconstruct / ReconstructData calls through one process-wide batcher over all visible GPUs (blb_rs.h:
 // blbrs_batcher_new): concurrent degraded reads (client/blb/reconstruct.go with
 // ReconstructBehavior.MaxInFlight > 1) and the increments of concurrent RSEncode RPCs
-// (internal/tractserver/store.go:1099) then share kernel launches.  Verify is never batched.
+// (internal/tractserver/store.go:1099, and reconstructAndVerify's Reconstruct + Verify at
+// :1132-1142) then share kernel launches.
 // Call once at process start-up, before coding begins; windowMicros = 0 batches naturally
 // (no added wait for a lone caller).
 func EnableBatching(maxBatch, windowMicros int) error {

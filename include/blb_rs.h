@@ -266,13 +266,14 @@ int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_s
  * of `length`-byte pieces), up to MaxInFlight (:19,35-45) at once; the tractserver calls
  * Encode once per 4 MiB increment of each RSEncode RPC (store.go:1099), up to
  * RejectCtlReqThreshold = 1000 RPCs at once (internal/tractserver/config.go:91).  A batcher
- * collects concurrent host Encode / Reconstruct / ReconstructData calls that arrive within
- * window_us (or until max_batch wait) and runs them as one kernel launch per (encoder shape,
- * plan, length) group plus one stream sync.  Attach it to an encoder and the plain
- * blbrs_encode / blbrs_reconstruct / blbrs_reconstruct_data calls on that encoder go through
- * it: same arguments, results and errors, the caller still blocks until its own stripe is
- * done -- the Go Encoder interface is unchanged.  (blbrs_verify and blbrs_reconstruct_verify
- * are never batched.)  window_us = 0 batches naturally: a free lane takes whatever is
+ * collects concurrent host Encode / Verify / Reconstruct / ReconstructData /
+ * reconstructAndVerify calls that arrive within window_us (or until max_batch wait) and runs
+ * them as one kernel launch per (encoder shape, plan, length) group -- plus the verify pass
+ * and its per-stripe flags for the verifying calls -- and one stream sync.  Attach it to an
+ * encoder and the plain blbrs_encode / blbrs_verify / blbrs_reconstruct /
+ * blbrs_reconstruct_data / blbrs_reconstruct_verify calls on that encoder go through it: same
+ * arguments, results and errors, the caller still blocks until its own stripe is done -- the
+ * Go Encoder interface is unchanged.  window_us = 0 batches naturally: a free lane takes whatever is
  * queued at once and calls arriving while the lanes are busy form the next batch, so a lone
  * caller does not wait; a positive window holds a batch open up to window_us after its first
  * call.

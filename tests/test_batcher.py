@@ -92,7 +92,10 @@ def test_batched_errors_unchanged():
     b.close()
 
 
-def test_batched_large_and_reconstruct_verify_not_batched():
+def test_batched_large_and_reconstruct_verify():
+    """A 1 MiB + 13 stripe with four erasures, then reconstructAndVerify
+    (internal/tractserver/store.go:1132-1142) through the batcher: decode and verify run as
+    one group (one sync), a good stripe verifies, a corrupted survivor does not."""
     k, m = 10, 4
     rng = np.random.default_rng(3)
     st = _stripe(rng, k, m, (1 << 20) + 13)
@@ -104,8 +107,58 @@ def test_batched_large_and_reconstruct_verify_not_batched():
     for i in (0, 3, 11, 13):
         assert np.array_equal(shards[i], st[i]), i
     shards = [None if i in (5,) else st[i] for i in range(k + m)]
-    assert enc.ReconstructAndVerify(shards)     # store.go path: never batched
-    assert b.stats() == (1, 1)
+    assert enc.ReconstructAndVerify(shards)
+    assert np.array_equal(shards[5], st[5])
+    bad = [None if i in (5,) else st[i].copy() for i in range(k + m)]
+    bad[12][777] ^= 0x40   # a surviving parity shard is wrong: the re-encode disagrees
+    assert not enc.ReconstructAndVerify(bad)
+    assert enc.Verify(list(st)) and not enc.Verify(bad[:5] + [st[5]] + bad[6:])
+    assert b.stats() == (5, 5)
+    enc.SetBatcher(None)
+    b.close()
+
+
+def test_batched_concurrent_reconstruct_verify():
+    """The curator-driven recovery path under load: concurrent reconstructAndVerify calls
+    (RSEncode RPCs with an indexMap, store.go:1102) from 16 threads share launches; every
+    rebuilt shard equals the original and exactly the corrupted stripes fail to verify."""
+    torch = _torch()
+    k, m, S = 6, 3, 300_001
+    rng = np.random.default_rng(11)
+    stripes = [_stripe(rng, k, m, S) for _ in range(4)]
+    b = reedsolomon.Batcher(max_batch=32, window_us=0)
+    enc = reedsolomon.New(k, m)
+    enc.SetBatcher(b)
+    errors = []
+
+    def server(tid):
+        for it in range(4):
+            full = stripes[(tid + it) % len(stripes)]
+            lost = [1 + it % 2, k + 1]   # a failed tractserver: the same slots for many chunks
+            corrupt = (tid + it) % 3 == 0
+            pinned = (tid + it) % 2 == 0
+            mk = (lambda a: torch.from_numpy(a.copy()).pin_memory().numpy()) if pinned else (lambda a: a.copy())
+            sh = [None if i in lost else mk(full[i]) for i in range(k + m)]
+            if corrupt:
+                victim = next(i for i in range(k + m) if i not in lost)
+                sh[victim][S // 2] ^= 0x01
+            try:
+                ok = enc.ReconstructAndVerify(sh)
+                assert ok == (not corrupt), (tid, it, ok)
+                if not corrupt:
+                    for i in lost:
+                        assert np.array_equal(sh[i], full[i]), (tid, it, i)
+            except Exception as e:  # noqa: BLE001 -- collected and re-raised on the main thread
+                errors.append(e)
+
+    ths = [threading.Thread(target=server, args=(t,)) for t in range(16)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors[:3]
+    reqs, launches = b.stats()
+    assert reqs == 16 * 4 and launches < reqs, (reqs, launches)
     enc.SetBatcher(None)
     b.close()
 
@@ -149,11 +202,13 @@ def test_batched_concurrent_encodes_match_oracle():
     reqs, launches = b.stats()
     assert reqs == 16 * 6
     assert launches < reqs, (reqs, launches)
-    # Errors keep their types on the batched path; Verify is never batched.
+    # Errors keep their types on the batched path; Verify goes through the batcher too.
     with pytest.raises(reedsolomon.ErrShardSize):
         enc.Encode([data[4096][0][:4095]] + [x.copy() for x in data[4096][1:]] + [np.zeros(4096, np.uint8)] * m)
     ok_shards = [x.copy() for x in data[4096]] + [x.copy() for x in want[4096]]
     assert enc.Verify(ok_shards)
-    assert b.stats()[0] == reqs
+    ok_shards[k][0] ^= 1
+    assert not enc.Verify(ok_shards)
+    assert b.stats()[0] == reqs + 2
     enc.SetBatcher(None)
     b.close()

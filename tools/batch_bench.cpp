@@ -2,11 +2,13 @@
 //   reconstruct (default): client degraded reads -- T threads x R calls
 //     of ReconstructData on RS(6,3) stripes of L-byte pinned pieces, one missing data shard, a
 //     fresh encoder per call (client/blb/reconstruct.go:172);
+//   rverify: the recovery RPCs' reconstructAndVerify (store.go:1132-1142), one data shard
+//     missing, as reconstruct (the random bytes never verify; the work is the same);
 //   encode: concurrent RSEncode RPCs (§8f row 1) -- T threads x R calls of Encode on RS(6,3)
 //     stripes of L-byte pinned increments (store.go:1099; EncodeIncrementSize 4 MiB, 1 MiB in
 //     tests), one encoder per RPC.
 // No Python in the loop.
-//   build: see tools/Makefile (target batch_bench); run: tools/_build/batch_bench [T] [R] [encode]
+//   build: see tools/Makefile (target batch_bench); run: tools/_build/batch_bench [T] [R] [encode|rverify]
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -30,6 +32,7 @@ int main(int argc, char** argv) {
     const int T = argc > 1 ? std::atoi(argv[1]) : 64;
     const int R = argc > 2 ? std::atoi(argv[2]) : 50;
     const bool encode = argc > 3 && std::strcmp(argv[3], "encode") == 0;
+    const bool rverify = argc > 3 && std::strcmp(argv[3], "rverify") == 0;  // reconstructAndVerify
     const int k = 6, m = 3, n = k + m;
     {  // cost of the per-shard pointer classification under T-way contention
         uint8_t* p = nullptr;
@@ -72,6 +75,11 @@ int main(int argc, char** argv) {
                         for (int i = 0; i < n; ++i) sh[i] = bufs[static_cast<size_t>(t) * (n + 1) + i];
                         if (encode) {
                             check(blbrs_encode(enc, sh.data(), lens.data()), "encode");
+                        } else if (rverify) {  // store.go:1132-1142; the bytes are random, so ok = 0
+                            sh[1] = bufs[static_cast<size_t>(t) * (n + 1) + n];
+                            lens[1] = 0;
+                            int ok = 0;
+                            check(blbrs_reconstruct_verify(enc, sh.data(), lens.data(), &ok), "reconstruct_verify");
                         } else {
                             sh[1] = bufs[static_cast<size_t>(t) * (n + 1) + n];  // output
                             lens[1] = 0;
@@ -98,7 +106,7 @@ int main(int argc, char** argv) {
                 std::printf("{\"op\": \"%s\", \"piece_bytes\": %zu, \"mode\": \"%s\", \"window_us\": %d, \"threads\": %d, "
                             "\"calls\": %.0f, \"calls_per_s\": %.0f, \"GiBps_data_read\": %.3f, \"us_per_call_latency\": %.1f, "
                             "\"calls_per_launch\": %.2f}\n",
-                            encode ? "encode" : "reconstruct_data", L, batched ? "batched" : "per_call", window_us, T, calls,
+                            encode ? "encode" : rverify ? "reconstruct_verify" : "reconstruct_data", L, batched ? "batched" : "per_call", window_us, T, calls,
                             calls / el,
                             calls * k * L / el / (1u << 30), el * 1e6 / R,
                             b ? static_cast<double>(r1 - r0) / static_cast<double>(l1 - l0 ? l1 - l0 : 1) : 1.0);
