@@ -123,16 +123,16 @@ def test_batched_concurrent_reconstruct_verify():
     (RSEncode RPCs with an indexMap, store.go:1102) from 16 threads share launches; every
     rebuilt shard equals the original and exactly the corrupted stripes fail to verify."""
     torch = _torch()
-    k, m, S = 6, 3, 300_001
+    k, m, S, T, R = 6, 3, 300_001, 16, 4
     rng = np.random.default_rng(11)
     stripes = [_stripe(rng, k, m, S) for _ in range(4)]
-    b = reedsolomon.Batcher(max_batch=32, window_us=0)
+    b = reedsolomon.Batcher(max_batch=32, window_us=2000)
     enc = reedsolomon.New(k, m)
     enc.SetBatcher(b)
-    errors = []
-
-    def server(tid):
-        for it in range(4):
+    # Every call's shards are built up front (pinning is slow), then the threads start together.
+    work = {}
+    for tid in range(T):
+        for it in range(R):
             full = stripes[(tid + it) % len(stripes)]
             lost = [1 + it % 2, k + 1]   # a failed tractserver: the same slots for many chunks
             corrupt = (tid + it) % 3 == 0
@@ -142,6 +142,14 @@ def test_batched_concurrent_reconstruct_verify():
             if corrupt:
                 victim = next(i for i in range(k + m) if i not in lost)
                 sh[victim][S // 2] ^= 0x01
+            work[tid, it] = (full, lost, corrupt, sh)
+    errors = []
+    start = threading.Barrier(T)
+
+    def server(tid):
+        start.wait()
+        for it in range(R):
+            full, lost, corrupt, sh = work[tid, it]
             try:
                 ok = enc.ReconstructAndVerify(sh)
                 assert ok == (not corrupt), (tid, it, ok)
@@ -151,14 +159,14 @@ def test_batched_concurrent_reconstruct_verify():
             except Exception as e:  # noqa: BLE001 -- collected and re-raised on the main thread
                 errors.append(e)
 
-    ths = [threading.Thread(target=server, args=(t,)) for t in range(16)]
+    ths = [threading.Thread(target=server, args=(t,)) for t in range(T)]
     for t in ths:
         t.start()
     for t in ths:
         t.join()
     assert not errors, errors[:3]
     reqs, launches = b.stats()
-    assert reqs == 16 * 4 and launches < reqs, (reqs, launches)
+    assert reqs == T * R and launches < reqs, (reqs, launches)
     enc.SetBatcher(None)
     b.close()
 
