@@ -228,6 +228,58 @@ def scale_extras(enc, k, m, S, world, rank, dev, dist):
     return out
 
 
+def host_call_extras(k, m, dev, threads=16, seconds=1.0):
+    """The tractserver's real call shape (rank 0 at N=1): `threads` concurrent RSEncode RPCs,
+    each calling Encode on one 4 MiB increment (EncodeIncrementSize, store.go:1099) of pool
+    buffers (rpc.GetBuffer -> blbrs_buffer_get, pinned, coded in place over PCIe), per call and
+    through a Batcher (window 0).  PCIe-inclusive; never the bench value."""
+    import threading
+    S = 4 << 20
+    out = {"threads": threads, "increment_bytes": S}
+    stripes = []
+    for t in range(threads):
+        sh = [rs.GetBuffer(S) for _ in range(k + m)]
+        g = np.random.default_rng(t)
+        for i in range(k):
+            sh[i][:] = g.integers(0, 256, S, dtype=np.uint8)
+        stripes.append(sh)
+    try:
+        for mode in ("per_call", "batched"):
+            enc = rs.New(k, m, devices=[dev.index])
+            b = rs.Batcher(max_batch=64, window_us=0, devices=[dev.index]) if mode == "batched" else None
+            if b is not None:
+                enc.SetBatcher(b)
+            for sh in stripes:
+                enc.Encode(sh)
+            counts = [0] * threads
+            stop = time.perf_counter() + seconds
+
+            def loop(t):
+                while time.perf_counter() < stop:
+                    enc.Encode(stripes[t])
+                    counts[t] += 1
+
+            t0 = time.perf_counter()
+            th = [threading.Thread(target=loop, args=(t,)) for t in range(threads)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            el = time.perf_counter() - t0
+            out[f"{mode}_GiBps_data"] = round(sum(counts) * k * S / GIB / el, 2)
+            if b is not None:
+                out["calls_per_launch"] = round(b.stats()[0] / max(1, b.stats()[1]), 2)
+                enc.SetBatcher(None)
+                b.close()
+        ok = all(enc.Verify(sh) for sh in stripes[:2])
+        out["verify_ok"] = bool(ok)
+    finally:
+        for sh in stripes:
+            for x in sh:
+                rs.PutBuffer(x)
+    return out
+
+
 def wide_fused_extras(S, dev):
     """Fused encode+CRC (65532-byte ChecksumFile blocks) against the plain encode of the same
     stripes for blb's widest class RS(12,5) and the bench's RS(10,4), B=512 each, interleaved
@@ -457,6 +509,7 @@ def main():
         extra.update(scale_extras(enc, k, m, S, world, rank, dev, dist))
         if world == 1:
             extra.update(wide_fused_extras(S, dev))
+            extra["host_calls_rs63_encode_4MiB_pool"] = host_call_extras(k, m, dev)
     if rank == 0 and world == 1 and not a.no_extra:
         cpu = cpu_baseline(k, m, a.cpu_seconds)
 
