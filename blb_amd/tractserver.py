@@ -95,10 +95,13 @@ class Store:
     """The RS slice of internal/tractserver.Store."""
 
     def __init__(self, talker: TractserverTalker, encode_increment_size: int = ENCODE_INCREMENT_PROD,
-                 pipeline: bool = False):
+                 pipeline: bool = False, batcher: Optional["reedsolomon.Batcher"] = None):
         self.tt = talker
         self.encode_increment_size = int(encode_increment_size)
         self.pipeline = pipeline
+        # Shared by the Stores of one process (rsgpu.EnableBatching): the Encode / Reconstruct
+        # / Verify calls of concurrent RSEncode RPCs share kernel launches (DESIGN §4d).
+        self.batcher = batcher
         self._pool = ThreadPoolExecutor(max_workers=32)
         self.local: dict[TractID, tuple] = {}   # tract id -> (device bytes, version)
 
@@ -158,6 +161,8 @@ class Store:
             enc = reedsolomon.New(N, M)
         except reedsolomon.RSError:
             return Error.ErrInvalidArgument
+        if self.batcher is not None:
+            enc.SetBatcher(self.batcher)
         windows = []
         off = 0
         while length > 0:

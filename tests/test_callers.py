@@ -196,6 +196,56 @@ def test_store_reconstruct_like_TestRSReconstruct(pipeline, oracle_lib):
 
 
 @pytest.mark.gpu
+def test_store_concurrent_rpcs_with_batcher(oracle_lib):
+    """Concurrent RSEncode RPCs (encode and indexMap recovery, half of them pipelined) on
+    Stores sharing one Batcher: every RPC writes the oracle's bytes, and the increments of
+    different RPCs share launches."""
+    import threading
+
+    from blb_amd import reedsolomon
+    N, M, B, inc, R = 6, 3, 150_000, 32768, 12
+    b = reedsolomon.Batcher(max_batch=64, window_us=0)
+    jobs = []
+    for r in range(R):
+        rng = np.random.default_rng(1000 + r)
+        data = [rng.integers(0, 256, B, dtype=np.uint8) for _ in range(N)] + [np.zeros(B, np.uint8) for _ in range(M)]
+        oracle_lib.encode(N, M, data)
+        t = MemTractserverTalker()
+        a = addrs(N + M)
+        recover = r % 3 == 2
+        srcs = [i for i in range(N + M) if i not in (1, 7)][:N] if recover else list(range(N))
+        dsts = [1, 7] if recover else list(range(N, N + M))
+        for lo in range(0, B, inc):
+            for i in srcs:
+                t.add_ctl_read_reply(a[i].host, data[i][lo:lo + inc], Error.ErrEOF)
+            for i in dsts:
+                t.add_ctl_write_reply(a[i].host, Error.NoError)
+        imap = srcs + dsts if recover else None
+        jobs.append((Store(t, encode_increment_size=inc, pipeline=r % 2 == 1, batcher=b), t, a, data, srcs, dsts, imap))
+    errs = [None] * R
+    start = threading.Barrier(R)
+
+    def rpc(r):
+        s, t, a, data, srcs, dsts, imap = jobs[r]
+        start.wait()
+        errs[r] = s.rs_encode(CID, B, [a[i] for i in srcs], [a[i] for i in dsts], imap)
+
+    th = [threading.Thread(target=rpc, args=(r,)) for r in range(R)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert errs == [Error.NoError] * R
+    for r, (s, t, a, data, srcs, dsts, imap) in enumerate(jobs):
+        for i in dsts:
+            got = np.concatenate([w[2] for w in t.ctl_write_calls[a[i].host]])
+            assert np.array_equal(got, data[i]), (r, i)
+    reqs, launches = b.stats()
+    assert launches < reqs, (reqs, launches)
+    b.close()
+
+
+@pytest.mark.gpu
 def test_store_reconstruct_verify_failure_is_unknown(oracle_lib):
     """reconstructAndVerify (store.go:1132-1142): with exactly k sources the rebuilt stripe
     is always a codeword, so Verify can only fail when an extra present shard disagrees;
