@@ -598,7 +598,8 @@ static void TestPackThenRSEncode(T* t) {
 // different RPCs must have shared launches.
 static void TestRSEncodeConcurrentBatched(T* t) {
     const int N = 6, M = 3, B = 200000, inc = 65536, R = 12;
-    if (reedsolomon::EnableBatching(64, 0) != reedsolomon::Err::None) Fatalf("EnableBatching failed");
+    // A 1 ms window so that the RPCs' increments reliably meet (sharing is checked below).
+    if (reedsolomon::EnableBatching(64, 1000) != reedsolomon::Err::None) Fatalf("EnableBatching failed");
     std::vector<std::vector<Bytes>> data(R);
     std::vector<std::unique_ptr<memTractserverTalker>> talkers;
     std::vector<std::vector<core::TSAddr>> addrs(R);

@@ -204,7 +204,9 @@ def test_store_concurrent_rpcs_with_batcher(oracle_lib):
 
     from blb_amd import reedsolomon
     N, M, B, inc, R = 6, 3, 150_000, 32768, 12
-    b = reedsolomon.Batcher(max_batch=64, window_us=0)
+    # A 2 ms window: the RPCs' Python-side gathers and scatters hold the GIL between calls,
+    # so without one, calls rarely meet (sharing is what this test checks).
+    b = reedsolomon.Batcher(max_batch=64, window_us=2000)
     jobs = []
     for r in range(R):
         rng = np.random.default_rng(1000 + r)
