@@ -37,6 +37,7 @@ SIGNATURES = {
     "blbrs_encode_crc_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _SZ, _P, _P]),
     "blbrs_crc32c_dev_at": (_I, [_P, _SZ, _SZ, _SZ, _SZ, _SZ, _P, _P, _P]),
     "blbrs_encode_crc_dev_at": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _SZ, _SZ, _P, _P, _P]),
+    "blbrs_reconstruct_crc_dev_at": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P, _I, _SZ, _SZ, _P, _P, _P]),
     "blbrs_pack_dev": (_I, [_P, _SZ, _SZ, _SZ, _P, _SZ, _P]),
     "blbrs_pack_encode_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P, _SZ, _P]),
     "blbrs_batcher_new": (_I, [_I, _I, ctypes.POINTER(_P)]),

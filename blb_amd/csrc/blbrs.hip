@@ -1291,12 +1291,11 @@ int blbrs_encode_crc_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stri
                                    crc_out_dev, stream);
 }
 
-int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
-                            size_t batch, size_t shard_len, size_t block, size_t phase, const uint32_t* seeds_dev,
-                            uint32_t* crc_out_dev, void* stream) {
-    if (!enc || !crc_out_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
-    if (batch == 0 || shard_len == 0) return BLBRS_OK;
-    if (batch > 0x7FFFFFFFull) return fail(BLBRS_ERR_INVALID_ARG, "batch too large");
+// Coding pass of plan `hp` (encode or decode) fused with the CRC-32C of its output rows:
+// crc[(j * batch + b) * nblocks + i] for output row j (hp->out_idx order).
+static int code_crc_dev(blbrs_encoder* enc, const std::string& key, const HostPlan& hp, uint8_t* stripes,
+                        size_t shard_stride, size_t stripe_stride, size_t batch, size_t shard_len, size_t block,
+                        size_t phase, const uint32_t* seeds_dev, uint32_t* crc_out_dev, void* stream) {
     if (block == 0) {
         block = shard_len;
         phase = 0;
@@ -1307,9 +1306,8 @@ int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_s
     if (rc) return rc;
     DevCall dc;
     if ((rc = dc.enter(stripes))) return rc;
-    auto hp = enc->encode_plan();
     const DevPlan* plan = nullptr;
-    if ((rc = enc->dev_plan("E", *hp, dc.dev, &plan))) return rc;
+    if ((rc = enc->dev_plan(key, hp, dc.dev, &plan))) return rc;
     if (block > shard_len + phase) block = shard_len + phase;  // one block
     const hipStream_t s = static_cast<hipStream_t>(stream);
     if (plan->passes.size() == 1) {
@@ -1336,16 +1334,41 @@ int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_s
         }
     }
     // Shapes without a fused instantiation (or unaligned): the coding pass, then the CRC of
-    // each parity row -- same results, one more read of the parity.
+    // each output row -- same results, one more read of the outputs.
     if ((rc = run_plan(*plan, st, batch, shard_len, Mode::kStore, nullptr, s))) return rc;
     const size_t nblocks = (shard_len + phase + block - 1) / block;
-    for (int j = 0; j < enc->m; ++j) {
-        const hipError_t e = crc32c_blocks(stripes + static_cast<size_t>(enc->k + j) * shard_stride, stripe_stride,
+    for (size_t j = 0; j < hp.out_idx.size(); ++j) {
+        const hipError_t e = crc32c_blocks(stripes + static_cast<size_t>(hp.out_idx[j]) * shard_stride, stripe_stride,
                                            batch, shard_len, block, phase, seeds_dev ? seeds_dev + j * batch : nullptr,
                                            crc_out_dev + j * batch * nblocks, s);
         if (e != hipSuccess) return hip_fail(e, "crc32c_blocks");
     }
     return BLBRS_OK;
+}
+
+int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                            size_t batch, size_t shard_len, size_t block, size_t phase, const uint32_t* seeds_dev,
+                            uint32_t* crc_out_dev, void* stream) {
+    if (!enc || !crc_out_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    if (batch == 0 || shard_len == 0) return BLBRS_OK;
+    if (batch > 0x7FFFFFFFull) return fail(BLBRS_ERR_INVALID_ARG, "batch too large");
+    auto hp = enc->encode_plan();
+    return code_crc_dev(enc, "E", *hp, stripes, shard_stride, stripe_stride, batch, shard_len, block, phase, seeds_dev,
+                        crc_out_dev, stream);
+}
+
+int blbrs_reconstruct_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                                 size_t batch, size_t shard_len, const uint8_t* present, int data_only, size_t block,
+                                 size_t phase, const uint32_t* seeds_dev, uint32_t* crc_out_dev, void* stream) {
+    if (!enc || !crc_out_dev) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    std::shared_ptr<HostPlan> hp;
+    std::string key;
+    bool nothing = false;
+    int rc = dev_decode_plan(enc, present, data_only, &hp, &key, &nothing);
+    if (rc || nothing || batch == 0 || shard_len == 0) return rc;
+    if (batch > 0x7FFFFFFFull) return fail(BLBRS_ERR_INVALID_ARG, "batch too large");
+    return code_crc_dev(enc, key, *hp, stripes, shard_stride, stripe_stride, batch, shard_len, block, phase, seeds_dev,
+                        crc_out_dev, stream);
 }
 
 int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {

@@ -338,6 +338,37 @@ class Encoder:
         _check(self._lib.blbrs_reconstruct_dev(self._h, stripes.data_ptr(), ss, bs, B, S, pres,
                                                int(data_only), st))
 
+    def ReconstructBatchCRC(self, stripes, present: Sequence[bool], block: int = 0, data_only: bool = False,
+                            stream: Optional[int] = None, phase: int = 0, seeds=None):
+        """ReconstructBatch fused with the CRC-32C of every rebuilt shard (the recovery RPC's
+        CtlWrite of the rebuilt pieces, store.go:1110-1120).  Returns [r, B, nblocks] int32
+        (r = rebuilt shards: missing data ascending, then missing parity unless data_only), or
+        None when nothing is rebuilt.  block / phase / seeds ([r, B] int32) as EncodeBatchCRC."""
+        import torch
+        B, S, ss, bs = self._stripes(stripes)
+        if len(present) != self.Shards:
+            raise ErrTooFewShards("too few shards given")
+        rows = [i for i in range(self.Shards) if not present[i] and (i < self.DataShards or not data_only)]
+        if not rows:
+            return None
+        if block <= 0:
+            blk, phase = S, 0
+        else:
+            blk = block
+        nblocks = (S + phase + blk - 1) // blk if S else 0
+        out = torch.empty((len(rows), B, nblocks), dtype=torch.int32, device=stripes.device)
+        sp = None
+        if seeds is not None:
+            if not (_is_torch(seeds) and seeds.dtype == torch.int32 and seeds.is_contiguous()
+                    and tuple(seeds.shape) == (len(rows), B) and seeds.device == stripes.device):
+                raise ErrInvalidArgument("seeds must be a contiguous [r, B] int32 tensor on the stripes' device")
+            sp = seeds.data_ptr()
+        pres = (ctypes.c_uint8 * self.Shards)(*[1 if p else 0 for p in present])
+        st = _torch_stream(stripes) if stream is None else stream
+        _check(self._lib.blbrs_reconstruct_crc_dev_at(self._h, stripes.data_ptr(), ss, bs, B, S, pres,
+                                                      int(data_only), blk, phase, sp, out.data_ptr(), st))
+        return out
+
     def VerifyBatch(self, stripes, stream: Optional[int] = None):
         """Returns a [B] torch.bool CUDA tensor: True where the stripe's parity is consistent."""
         import torch

@@ -259,6 +259,17 @@ int blbrs_crc32c_dev_at(const uint8_t* data, size_t stride, size_t batch, size_t
 int blbrs_encode_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
                             size_t stripe_stride, size_t batch, size_t shard_len, size_t block,
                             size_t phase, const uint32_t* seeds_dev, uint32_t* crc_out_dev, void* stream);
+/* The recovery write path: blbrs_reconstruct_dev (one erasure pattern for the batch; the
+ * rebuilt shards go to the new hosts by CtlWrite, internal/tractserver/store.go:1110-1120)
+ * fused with the CRC-32C of every rebuilt shard, the same block / phase / seed rules as
+ * blbrs_encode_crc_dev_at.  Output row j = the j-th rebuilt shard: missing data shards
+ * ascending, then (data_only == 0) missing parity shards ascending;
+ * crc_out_dev[(j * batch + b) * nblocks + i], seeds_dev[j * batch + b].  Nothing missing (or
+ * data_only with only parity missing): no work, no CRC written. */
+int blbrs_reconstruct_crc_dev_at(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
+                                 size_t stripe_stride, size_t batch, size_t shard_len,
+                                 const uint8_t* present, int data_only, size_t block, size_t phase,
+                                 const uint32_t* seeds_dev, uint32_t* crc_out_dev, void* stream);
 
 /* ---- batched host calls: client reconstructs and tractserver encodes (SURVEY.md §8f rows
  * 4 and 1) ----

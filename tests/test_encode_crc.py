@@ -213,3 +213,47 @@ def test_encode_crc_at_rejects_bad_phase():
     st = torch.zeros((1, 9, 8192), dtype=torch.uint8, device="cuda")
     with pytest.raises(rs.ErrInvalidArgument):
         enc.EncodeBatchCRC(st, 65532, phase=65532)
+
+
+@pytest.mark.parametrize("k,m,lost,data_only", [(6, 3, (1,), True), (6, 3, (0, 7), False), (10, 4, (1, 7), False),
+                                                (12, 5, (2, 5, 13, 16), False), (12, 5, (3, 15), True),
+                                                (5, 5, (0, 6), False), (3, 2, (1, 3), False)])
+def test_reconstruct_crc_vs_oracle(oracle_lib, k, m, lost, data_only):
+    """blbrs_reconstruct_crc_dev_at: the recovery RPC rebuilds the missing pieces and the
+    receiver checksums them (store.go:1110-1120, pkg/disk/checksum_block.go:76-81).  Rebuilt
+    bytes equal the originals; each rebuilt shard's block CRCs (file-aligned phase, seeded
+    first block) equal the oracle's; survivors untouched.  (5,5) has no fused instantiation
+    and runs the two-pass fallback."""
+    O = oracle_lib
+    rng = np.random.default_rng(7 * k + m + len(lost))
+    enc = rs.New(k, m)
+    present = [i not in lost for i in range(k + m)]
+    rows = [i for i in sorted(lost) if i < k or not data_only]
+    for S, block, phase in ((4128704, 65532, 256), (1 << 20, 0, 0), (200000, 4096, 4092), (70001, 65532, 1000)):
+        B = 2
+        full = np.empty((B, k + m, S), np.uint8)
+        for b in range(B):
+            sh = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+            O.encode(k, m, sh, use_avx2=True, threads=8)
+            full[b] = np.stack(sh)
+        host = full.copy()
+        host[:, list(lost)] = 0xC3
+        dev = torch.from_numpy(host).cuda()
+        seeds_h = rng.integers(0, 1 << 32, (len(rows), B), dtype=np.uint64).astype(np.uint32)
+        seeds = torch.from_numpy(seeds_h.view(np.int32)).cuda() if block else None
+        crc = enc.ReconstructBatchCRC(dev, present, block, data_only=data_only, phase=phase, seeds=seeds)
+        crc = crc.cpu().numpy().view(np.uint32)
+        got = dev.cpu().numpy()
+        blk = block or S
+        assert crc.shape[0] == len(rows)
+        for b in range(B):
+            for i in range(k + m):
+                if i in lost and i not in rows:
+                    assert (got[b, i] == 0xC3).all(), (k, m, S, b, i, "untouched parity")
+                else:
+                    assert np.array_equal(got[b, i], full[b, i]), (k, m, S, b, i, "bytes")
+            for j, i in enumerate(rows):
+                want = _expected_blocks_at(O, full[b, i], blk, phase if block else 0, int(seeds_h[j, b]) if block else 0)
+                assert np.array_equal(crc[j, b], want), (k, m, S, block, phase, b, i, "crc")
+    assert enc.ReconstructBatchCRC(torch.zeros((1, k + m, 64), dtype=torch.uint8, device="cuda"),
+                                   [True] * (k + m), 65532) is None
