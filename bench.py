@@ -387,6 +387,19 @@ def main():
             "GiBps_data": round(B * k * S / GIB / (dec_ms * 1e-3), 2),
             "ms_per_launch": round(dec_ms, 3),
             "hbm_GBps_algorithmic": round(B * (k + 1) * S / (dec_ms * 1e-3) / 1e9, 1)}
+        # The recovery write path: the same rebuild fused with the ChecksumFile CRCs of the
+        # rebuilt shard (blbrs_reconstruct_crc_dev_at, 65532-byte blocks).
+        enc.ReconstructBatchCRC(stripes, present, 65532, data_only=True)
+        torch.cuda.synchronize(dev)
+        for s, e in dev_evs:
+            s.record(stream)
+            enc.ReconstructBatchCRC(stripes, present, 65532, data_only=True)
+            e.record(stream)
+        torch.cuda.synchronize(dev)
+        rc_ms = float(np.mean([s.elapsed_time(e) for s, e in dev_evs]))
+        extra["reconstruct_crc_fused_1_data_erasure"] = {
+            "ms_per_launch": round(rc_ms, 3), "ratio_to_reconstruct": round(rc_ms / dec_ms, 3), "block": 65532,
+            "hbm_GBps_algorithmic": round(B * (k + 1) * S / (rc_ms * 1e-3) / 1e9, 1)}
         # Verify (reconstructAndVerify's parity recompute + compare, store.go:1136), fused.
         ver_evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(max(3, a.steps // 2))]
