@@ -312,6 +312,94 @@ def wide_fused_extras(S, dev):
     return out
 
 
+def _ev_ms(fn, reps, stream, dev):
+    """Mean HIP-event time (ms) of `reps` calls of fn on `stream` (one event pair per call)."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for s, e in evs:
+        s.record(stream)
+        fn()
+        e.record(stream)
+    torch.cuda.synchronize(dev)
+    return float(np.mean([s.elapsed_time(e) for s, e in evs]))
+
+
+def cold_class_extras(S, dev, batch=512, reps=4):
+    """blb's COLD transition class RS(8,3) (targetClass, internal/curator/
+    storage_class_loop.go:41-44), B=512 stripes of 8 MiB (rank 0 at N=1): Encode, 1- and
+    2-erasure Reconstruct, Encode fused with the ChecksumFile CRCs of a parity window at file
+    offset 4 MiB (phase 256, seeded), and PackTracts fused with Encode.  Each row carries its
+    algorithmic HBM bytes per launch and the fraction of the 8 TB/s spec."""
+    from blb_amd import pack
+    k, m = 8, 3
+    n = k + m
+    stream = torch.cuda.current_stream(dev)
+    st = torch.empty((batch, n, S), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(8303)
+    st[:, :k].random_(0, 256, generator=g)
+    e = rs.New(k, m)
+    out = {"workload": f"RS(8,3), batch={batch} stripes of {S >> 20} MiB"}
+
+    def row(name, ms, nbytes, **kw):
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[name] = {"ms_per_launch": round(ms, 3), "hbm_GBps_algorithmic": round(gbs, 1),
+                     "frac_of_8TBps": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": nbytes, **kw}
+
+    e.EncodeBatch(st)
+    torch.cuda.synchronize(dev)
+    enc_ms = _ev_ms(lambda: e.EncodeBatch(st), reps, stream, dev)
+    ok = bool(e.VerifyBatch(st).all())
+    row("encode", enc_ms, batch * n * S, GiBps_data=round(batch * k * S / GIB / (enc_ms * 1e-3), 1), verify_ok=ok)
+    ref = st[:, 1].clone()
+    pres1 = [i != 1 for i in range(n)]
+    st[:, 1].fill_(0xA5)
+    e.ReconstructBatch(st, pres1, data_only=True)
+    r1_ok = bool(torch.equal(st[:, 1], ref))
+    r1_ms = _ev_ms(lambda: e.ReconstructBatch(st, pres1, data_only=True), reps, stream, dev)
+    row("reconstruct_1_data_erasure", r1_ms, batch * (k + 1) * S, restored=r1_ok)
+    pres2 = [i not in (1, 5) for i in range(n)]
+    ref5 = st[:, 5].clone()
+    st[:, 1].fill_(0x5A)
+    st[:, 5].fill_(0xC3)
+    e.ReconstructBatch(st, pres2)
+    r2_ok = bool(torch.equal(st[:, 1], ref)) and bool(torch.equal(st[:, 5], ref5))
+    r2_ms = _ev_ms(lambda: e.ReconstructBatch(st, pres2), reps, stream, dev)
+    row("reconstruct_2_data_erasures", r2_ms, batch * (k + 2) * S, restored=r2_ok)
+    del ref, ref5
+    # rsEncodeOne's parity window 1 (file offset 4 MiB: phase 4 MiB mod 65532 = 256), seeded
+    # with the CRC of the partial block window 0 left (crc32.Update, checksum_block.go:76-81).
+    seeds = torch.randint(-2**31, 2**31 - 1, (m, batch), dtype=torch.int32, device=dev)
+    e.EncodeBatchCRC(st, 65532, phase=256, seeds=seeds)
+    torch.cuda.synchronize(dev)
+    fc_ms = _ev_ms(lambda: e.EncodeBatchCRC(st, 65532, phase=256, seeds=seeds), reps, stream, dev)
+    row("encode_crc_fused_b65532_phase256", fc_ms, batch * n * S, ratio_to_encode=round(fc_ms / enc_ms, 3),
+        verify_ok=bool(e.VerifyBatch(st).all()))
+    # PackTracts + Encode: tracts of 64 KiB..8 MiB from a 4 GiB device pool at padToLength-
+    # aligned offsets into the B*k data pieces (the main bench's extent generator).
+    pool = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev)
+    prng = np.random.default_rng(83)
+    ext, read_bytes = [], 0
+    for p in range(batch * k):
+        off = 0
+        while True:
+            ln = int(prng.integers(64 << 10, (8 << 20) + 1))
+            if off + ln > S:
+                break
+            src = int(prng.integers(0, pool.numel() - ln))
+            ext.append((pool[src:], off, ln, p))
+            read_bytes += ln
+            off += pack.padded_length(ln)
+    pack.PackEncode(e, st, ext)
+    torch.cuda.synchronize(dev)
+    torch.cuda._sleep(400_000_000)  # keeps the host-side extent checks outside the window
+    pe_ms = _ev_ms(lambda: pack.PackEncode(e, st, ext), 1, stream, dev)
+    row("pack_encode_fused", pe_ms, read_bytes + batch * n * S, bytes_read=read_bytes,
+        tracts=len(ext), verify_ok=bool(e.VerifyBatch(st).all()))
+    del st, pool, ext
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = parse()
     r = multigpu.env_rank()
@@ -522,6 +610,7 @@ def main():
         extra.update(scale_extras(enc, k, m, S, world, rank, dev, dist))
         if world == 1:
             extra.update(wide_fused_extras(S, dev))
+            extra["cold_class_rs83_b512"] = cold_class_extras(S, dev)
             extra["host_calls_rs63_encode_4MiB_pool"] = host_call_extras(k, m, dev)
     if rank == 0 and world == 1 and not a.no_extra:
         cpu = cpu_baseline(k, m, a.cpu_seconds)

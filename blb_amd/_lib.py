@@ -54,6 +54,10 @@ SIGNATURES = {
     "blbrs_buffer_get": (_I, [_SZ, ctypes.POINTER(_P), ctypes.POINTER(_SZ)]),
     "blbrs_buffer_put": (_I, [_P]),
     "blbrs_pool_set_idle_limit": (_I, [_SZ]),
+    "blbrs_buffer_register": (_I, [_P, _SZ]),
+    "blbrs_buffer_unregister": (_I, [_P]),
+    "blbrs_pool_set_live_limit": (_I, [_SZ]),
+    "blbrs_encoder_lane_stats": (_I, [_P, _I, _P]),
     "blbrs_get_pool_stats": (_I, [_P]),
     "blbrs_host_alloc": (_I, [_SZ, ctypes.POINTER(_P)]),
     "blbrs_host_free": (_I, [_P]),
@@ -80,7 +84,15 @@ class DeviceStats(ctypes.Structure):
 class PoolStats(ctypes.Structure):
     """blbrs_pool_stats"""
     _fields_ = [("gets", ctypes.c_uint64), ("puts", ctypes.c_uint64), ("allocs", ctypes.c_uint64),
-                ("frees", ctypes.c_uint64), ("live_bytes", ctypes.c_uint64), ("idle_bytes", ctypes.c_uint64)]
+                ("frees", ctypes.c_uint64), ("live_bytes", ctypes.c_uint64), ("idle_bytes", ctypes.c_uint64),
+                ("registered_bytes", ctypes.c_uint64), ("registrations", ctypes.c_uint64),
+                ("live_limit", ctypes.c_uint64), ("limit_rejects", ctypes.c_uint64)]
+
+
+class LaneStats(ctypes.Structure):
+    """blbrs_lane_stats"""
+    _fields_ = [("calls", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("inflight_calls", ctypes.c_int64),
+                ("inflight_bytes", ctypes.c_int64)]
 
 
 class DevPart(ctypes.Structure):
@@ -101,7 +113,12 @@ def load() -> ctypes.CDLL:
                 f"blb_amd: HIP engine library not built ({LIB_PATH} missing); run "
                 "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C blb_amd`")
         lib = ctypes.CDLL(LIB_PATH)
+        # An older build loaded through $BLBRS_LIB_PATH for an A/B run (tools/) may lack the
+        # newest entry points; the shipped library must export them all (tests/test_capi.py).
+        lenient = "BLBRS_LIB_PATH" in os.environ
         for name, (res, args) in SIGNATURES.items():
+            if lenient and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

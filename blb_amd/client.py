@@ -19,7 +19,7 @@ from typing import Optional, Protocol
 
 import numpy as np
 
-from . import reedsolomon
+from . import reedsolomon, rpc
 from .blbcore import RS_CHUNK_VERSION, Error, RSChunkID, StorageClass, TractID, rs_params
 
 
@@ -107,58 +107,70 @@ class Client:
 
     # reconstruct.go:65-195
     def reconstruct_one_tract(self, tract: TractPointer, thisB: np.ndarray, offset: int, length: int) -> TractResult:
-        with self._sem:
-            n, m = rs_params(StorageClass(tract.cls))
-            target, requests = -1, []
-            for i, host in enumerate(tract.other_hosts):
-                if tract.other_tsids[i] == tract.tsid:
-                    target = i
-                    continue
-                if host == "":
-                    continue
-                requests.append(i)
-            if target < 0:
-                return TractResult(len(thisB), 0, Error.ErrInvalidArgument)
-            if len(requests) < n:
-                return TractResult(len(thisB), 0, Error.ErrHostNotExist)
+        # reconstruct.go:126 `defer rpc.PutBuffer(p.res, true)` for each of the first n good
+        # replies; errored replies and stragglers are dropped to the collector (rpc.py).
+        kept: list = []
+        try:
+            with self._sem:
+                return self._reconstruct(tract, thisB, offset, length, kept)
+        finally:
+            for b in kept:
+                rpc.PutBuffer(b, True)
 
-            def fetch(i):
-                tid = tract.base_chunk.add(i).to_tract_id()
-                res, err = self.tractservers.read(tract.other_hosts[i], tid, RS_CHUNK_VERSION, length, offset)
-                if err in (Error.NoError, Error.ErrEOF) and (res is None or len(res) != length):
-                    err = Error.ErrShortRead
-                return i, res, err
+    def _reconstruct(self, tract: TractPointer, thisB: np.ndarray, offset: int, length: int,
+                     kept: list) -> TractResult:
+        n, m = rs_params(StorageClass(tract.cls))
+        target, requests = -1, []
+        for i, host in enumerate(tract.other_hosts):
+            if tract.other_tsids[i] == tract.tsid:
+                target = i
+                continue
+            if host == "":
+                continue
+            requests.append(i)
+        if target < 0:
+            return TractResult(len(thisB), 0, Error.ErrInvalidArgument)
+        if len(requests) < n:
+            return TractResult(len(thisB), 0, Error.ErrHostNotExist)
 
-            data: list = [None] * (n + m)
-            good, last_err = 0, Error.NoError
-            futs = [self._pool.submit(fetch, i) for i in requests]
-            for f in as_completed(futs):
-                i, res, err = f.result()
-                if err not in (Error.NoError, Error.ErrEOF):
-                    last_err = err
-                    continue
-                good += 1
-                data[i] = np.ascontiguousarray(res, dtype=np.uint8)
-                if good >= n:
-                    break
-            # Go cancels the context here (reconstruct.go:154): reads not started yet are
-            # dropped, running ones finish in the pool and their replies are ignored.
-            for f in futs:
-                f.cancel()
-            if good < n:
-                return TractResult(len(thisB), 0, last_err)
-            try:
-                enc = self._encoder(n, m)
-            except reedsolomon.RSError:
-                return TractResult(len(thisB), 0, Error.ErrInvalidArgument)
-            # data[targetIdx] = thisB[0:0:length]: output lands in the caller's buffer.
-            try:
-                enc.ReconstructData(data, outs={target: thisB})
-            except reedsolomon.RSError:
-                return TractResult(len(thisB), 0, Error.ErrCorruptData)
-            out = data[target]
-            if out is None or len(out) != length or out.ctypes.data != thisB.ctypes.data:
-                return TractResult(len(thisB), 0, Error.ErrCorruptData)
-            thisB[length:] = 0
-            self.reconstructs += 1
-            return TractResult(len(thisB), length, Error.ErrEOF if length < len(thisB) else Error.NoError)
+        def fetch(i):
+            tid = tract.base_chunk.add(i).to_tract_id()
+            res, err = self.tractservers.read(tract.other_hosts[i], tid, RS_CHUNK_VERSION, length, offset)
+            if err in (Error.NoError, Error.ErrEOF) and (res is None or len(res) != length):
+                err = Error.ErrShortRead
+            return i, res, err
+
+        data: list = [None] * (n + m)
+        good, last_err = 0, Error.NoError
+        futs = [self._pool.submit(fetch, i) for i in requests]
+        for f in as_completed(futs):
+            i, res, err = f.result()
+            if err not in (Error.NoError, Error.ErrEOF):
+                last_err = err
+                continue
+            good += 1
+            data[i] = np.ascontiguousarray(res, dtype=np.uint8)
+            kept.append(res)
+            if good >= n:
+                break
+        # Go cancels the context here (reconstruct.go:154): reads not started yet are
+        # dropped, running ones finish in the pool and their replies are ignored.
+        for f in futs:
+            f.cancel()
+        if good < n:
+            return TractResult(len(thisB), 0, last_err)
+        try:
+            enc = self._encoder(n, m)
+        except reedsolomon.RSError:
+            return TractResult(len(thisB), 0, Error.ErrInvalidArgument)
+        # data[targetIdx] = thisB[0:0:length]: output lands in the caller's buffer.
+        try:
+            enc.ReconstructData(data, outs={target: thisB})
+        except reedsolomon.RSError:
+            return TractResult(len(thisB), 0, Error.ErrCorruptData)
+        out = data[target]
+        if out is None or len(out) != length or out.ctypes.data != thisB.ctypes.data:
+            return TractResult(len(thisB), 0, Error.ErrCorruptData)
+        thisB[length:] = 0
+        self.reconstructs += 1
+        return TractResult(len(thisB), length, Error.ErrEOF if length < len(thisB) else Error.NoError)

@@ -383,43 +383,76 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             }
         }
     }
-    // Zero-copy: when every shard the steps touch is pinned (or device) memory, the kernels
-    // read and write it in place over PCIe -- no staging, and both link directions busy at
-    // once (RS(6,3): 50.8 GiB/s of data vs 37.3 through copy engines).
-    {
-        std::vector<uint64_t> view(batch * n, 0);
-        bool all = true;
-        for (size_t b = 0; b < batch && all; ++b)
-            for (int i = 0; i < n && all; ++i)
-                if (touched[i]) all = rt::device_view(shards[b * n + i], &view[b * n + i]);
-        if (all) {
-            Stripes st;
-            st.nshards = n;
-            if ((rc = w->upload_table(view.data(), view.size(), &st.ptrs, &st.aligned))) return rc;
-            if (verify) HIP_TRY(hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]));
-            for (size_t t = 0; t < steps.size(); ++t)
-                if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) {
-                    (void)hipStreamSynchronize(w->s[0]);
-                    return rc;
-                }
-            int32_t flag = 0;
-            if (verify) HIP_TRY(hipMemcpyAsync(&flag, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]));
-            HIP_TRY(hipStreamSynchronize(w->s[0]));
-            if (ok) *ok = flag ? 0 : 1;
-            return BLBRS_OK;
-        }
+    auto drain = [&](int rc_) {
+        (void)hipStreamSynchronize(w->s[0]);
+        (void)hipStreamSynchronize(w->s[1]);
+        return rc_;
+    };
+    // Per-slot addressing: pinned (or device) shards are read and written in place by the
+    // kernels -- zero copy, over PCIe for pinned host memory, both link directions busy at once
+    // (RS(6,3): 50.8 GiB/s of data vs 37.3 through copy engines) -- and only
+    // pageable shards go through the worker's staging ring.  blb's degraded read has k pool
+    // buffers in and the user's pageable Blob.ReadAt buffer out (client/blb/reconstruct.go:
+    // 172-173, blob.go:59): one staged slot, not k + 1.
+    std::vector<uint64_t> view(batch * n, 0);
+    std::vector<char> pageable(batch * n, 0);
+    int max_staged = 0;  // pageable touched slots of the worst stripe
+    for (size_t b = 0; b < batch; ++b) {
+        int ns = 0;
+        for (int i = 0; i < n; ++i)
+            if (touched[i] && !rt::device_view(shards[b * n + i], &view[b * n + i])) {
+                pageable[b * n + i] = 1;
+                ++ns;
+            }
+        max_staged = std::max(max_staged, ns);
     }
-    // Staged: column chunks of each stripe alternate over the worker's two streams and two
+    if (max_staged == 0) {
+        // Everything in place: one launch per step over the whole batch.
+        Stripes st;
+        st.nshards = n;
+        if ((rc = w->upload_table(view.data(), view.size(), &st.ptrs, &st.aligned))) return drain(rc);
+        hipError_t e = hipSuccess;
+        if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
+        if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
+        for (size_t t = 0; t < steps.size(); ++t)
+            if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
+        int32_t flag = 0;
+        if (verify) e = hipMemcpyAsync(&flag, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
+        const hipError_t f = hipStreamSynchronize(w->s[0]);
+        if (e == hipSuccess) e = f;
+        if (e != hipSuccess) return drain(hip_fail(e, "zero-copy call"));
+        if (ok) *ok = flag ? 0 : 1;
+        return BLBRS_OK;
+    }
+    // Staged: units of (stripe, column chunk) alternate over the worker's two streams and two
     // ring slots, so the H2D of unit u+1 overlaps the kernels and D2H of unit u.  A slot is
     // reused two units later on the same stream, i.e. after that unit's D2H -- in stream
-    // order, no event needed.  Device staging is bounded by 2 x kStageSlotBudget.
+    // order, no event needed.  A slot holds only the unit's pageable shards; the pointer table
+    // of every unit (staged shards -> their ring place, the rest -> their own memory at the
+    // chunk's column) is built up front and uploaded once.  Device staging is bounded by
+    // 2 x kStageSlotBudget.
     const size_t Sp = round_up(S, 256);
     size_t chunk = S;
-    if (S > (size_t{2} << 20) || static_cast<size_t>(n) * Sp > rt::kStageSlotBudget)
-        chunk = std::max<size_t>(4096, std::min<size_t>(size_t{1} << 20, rt::kStageSlotBudget / n / 256 * 256));
+    if (S > (size_t{2} << 20) || static_cast<size_t>(max_staged) * Sp > rt::kStageSlotBudget)
+        chunk = std::max<size_t>(4096,
+                                 std::min<size_t>(size_t{1} << 20, rt::kStageSlotBudget / max_staged / 256 * 256));
     const size_t cp = round_up(chunk, 256);
-    const size_t slot_bytes = static_cast<size_t>(n) * cp;
+    const size_t slot_bytes = static_cast<size_t>(max_staged) * cp;
     if ((rc = w->ensure_stage(2 * slot_bytes))) return rc;
+    const size_t per_stripe = (S + chunk - 1) / chunk, units = batch * per_stripe;
+    const uint64_t stage_view = reinterpret_cast<uint64_t>(w->stage);
+    std::vector<uint64_t> table(units * n, 0);
+    for (size_t b = 0, u = 0; b < batch; ++b)
+        for (size_t off = 0; off < S; off += chunk, ++u) {
+            const uint64_t slot = stage_view + (u & 1) * slot_bytes;
+            for (int i = 0, r = 0; i < n; ++i) {
+                if (!touched[i]) continue;
+                table[u * n + i] = pageable[b * n + i] ? slot + static_cast<uint64_t>(r++) * cp : view[b * n + i] + off;
+            }
+        }
+    const uint64_t* tab_dev = nullptr;
+    bool tab_aligned = false;
+    if ((rc = w->upload_table(table.data(), table.size(), &tab_dev, &tab_aligned))) return drain(rc);
     hipEvent_t ev = nullptr;
     struct EvFree {
         hipEvent_t& e;
@@ -427,16 +460,14 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             if (e) (void)hipEventDestroy(e);
         }
     } ev_free{ev};
-    auto drain = [&](int rc_) {
-        (void)hipStreamSynchronize(w->s[0]);
-        (void)hipStreamSynchronize(w->s[1]);
-        return rc_;
-    };
-    if (verify) {
-        HIP_TRY(hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]));
-        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(ev, w->s[0]));
-        HIP_TRY(hipStreamWaitEvent(w->s[1], ev, 0));
+    {
+        // s[1]'s units read the table (and, verifying, the zeroed flag) queued on s[0].
+        hipError_t e = hipSuccess;
+        if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(ev, w->s[0]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(w->s[1], ev, 0);
+        if (e != hipSuccess) return drain(hip_fail(e, "staged call setup"));
     }
     size_t u = 0;
     for (size_t b = 0; b < batch; ++b) {
@@ -446,29 +477,37 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             hipStream_t s = w->s[u & 1];
             uint8_t* slot = w->stage + (u & 1) * slot_bytes;
             hipError_t e = hipSuccess;
-            for (int i = 0; i < n && e == hipSuccess; ++i)
-                if (need_in[i]) e = hipMemcpyAsync(slot + i * cp, sh[i] + off, len, hipMemcpyHostToDevice, s);
+            for (int i = 0, r = 0; i < n && e == hipSuccess; ++i) {
+                if (!touched[i] || !pageable[b * n + i]) continue;
+                if (need_in[i]) e = hipMemcpyAsync(slot + r * cp, sh[i] + off, len, hipMemcpyHostToDevice, s);
+                ++r;
+            }
             if (e != hipSuccess) return drain(hip_fail(e, "H2D"));
             Stripes st;
-            st.base = slot;
-            st.shard_stride = cp;
-            st.stripe_stride = slot_bytes;
-            st.aligned = true;
+            st.ptrs = tab_dev + u * n;
+            st.nshards = n;
+            st.aligned = tab_aligned;
             for (size_t t = 0; t < steps.size(); ++t)
                 if ((rc = run_plan(*plans[t], st, 1, len, steps[t].mode, w->flag, s))) return drain(rc);
-            for (int i = 0; i < n && e == hipSuccess; ++i)
-                if (is_out[i]) e = hipMemcpyAsync(sh[i] + off, slot + i * cp, len, hipMemcpyDeviceToHost, s);
+            for (int i = 0, r = 0; i < n && e == hipSuccess; ++i) {
+                if (!touched[i] || !pageable[b * n + i]) continue;
+                if (is_out[i]) e = hipMemcpyAsync(sh[i] + off, slot + r * cp, len, hipMemcpyDeviceToHost, s);
+                ++r;
+            }
             if (e != hipSuccess) return drain(hip_fail(e, "D2H"));
         }
     }
     int32_t flag = 0;
+    hipError_t e = hipSuccess;
     if (verify) {
-        HIP_TRY(hipEventRecord(ev, w->s[1]));
-        HIP_TRY(hipStreamWaitEvent(w->s[0], ev, 0));
-        HIP_TRY(hipMemcpyAsync(&flag, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]));
+        e = hipEventRecord(ev, w->s[1]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(w->s[0], ev, 0);
+        if (e == hipSuccess) e = hipMemcpyAsync(&flag, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
     }
-    HIP_TRY(hipStreamSynchronize(w->s[0]));
-    HIP_TRY(hipStreamSynchronize(w->s[1]));
+    const hipError_t f0 = hipStreamSynchronize(w->s[0]);
+    const hipError_t f1 = hipStreamSynchronize(w->s[1]);
+    if (e == hipSuccess) e = f0 != hipSuccess ? f0 : f1;
+    if (e != hipSuccess) return drain(hip_fail(e, "staged call"));
     if (ok) *ok = flag ? 0 : 1;
     return BLBRS_OK;
 }
@@ -480,15 +519,25 @@ int host_call(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const
     int rc = enc->lanes(&lanes);
     if (rc) return rc;
     const int n = enc->k + enc->m;
+    // Device-memory shards pin the call to their device; they must all be on one device
+    // (a kernel dereferencing another GPU's HBM would need peer access).
     int dev = -1;
-    for (int i = 0; i < n && dev < 0; ++i) {
+    for (int i = 0; i < n; ++i) {
         uint64_t view = 0;
         int owner = -1;
-        if (shards[i] && rt::device_view(shards[i], &view, &owner) && owner >= 0) dev = owner;
+        if (shards[i] && rt::device_view(shards[i], &view, &owner) && owner >= 0) {
+            if (dev >= 0 && owner != dev) return fail(BLBRS_ERR_INVALID_ARG, "shards on different devices");
+            dev = owner;
+        }
     }
-    if (dev < 0) dev = lanes[rt::pick_lane(lanes, enc->rr)];
+    int occ = 0;
+    if (dev < 0) {
+        const size_t li = rt::pick_lane(lanes, enc->rr);
+        dev = lanes[li];
+        occ = rt::lane_keys(lanes)[li].second;
+    }
     rt::LoadTicket ticket;
-    ticket.take(dev);
+    ticket.take(dev, occ, static_cast<uint64_t>(n) * S);
     rt::DeviceGuard guard;
     if ((rc = guard.enter(dev))) return rc;
     return host_run(enc, steps, shards, 1, S, ok, dev);
@@ -686,8 +735,8 @@ struct blbrs_batcher {
 
     // Queue `r` (mu held): on its required device, else the device with the shortest queue.
     void enqueue(BatchReq* r) {
-        int dev = r->dev;
-        if (dev < 0 || !queues.count(dev)) {
+        int dev = r->dev;  // batched_call has checked that a required device has a queue
+        if (dev < 0) {
             const size_t start = rr.fetch_add(1) % devices.size();
             dev = devices[start];
             size_t best = queues[dev].q.size();
@@ -772,7 +821,7 @@ int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key, s
     } stage;
     if (nstaged) {
         size_t cap = 0;
-        int rc = rt::pool_get(nstaged * Sp, &stage.p, &cap);
+        int rc = rt::pool_get(nstaged * Sp, &stage.p, &cap, /*internal=*/true);
         if (rc) return rc;
         for (int i = 0; i < n; ++i) {
             if (slot[i] < 0) continue;
@@ -781,6 +830,9 @@ int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key, s
             if (!rt::device_view(p, &req.views[i])) return fail(BLBRS_ERR_HIP, "pinned staging has no device mapping");
         }
     }
+    if (req.dev >= 0 && !b->queues.count(req.dev))  // queues is fixed after make_batcher
+        return fail(BLBRS_ERR_INVALID_ARG, "shards live on device " + std::to_string(req.dev) +
+                                               ", which is not in the batcher's device list");
     req.arrival = std::chrono::steady_clock::now();
     {
         std::lock_guard<std::mutex> lk(b->mu);
@@ -891,6 +943,16 @@ int blbrs_encoder_devices(blbrs_encoder* enc, int* out, int cap, int* n) {
     *n = static_cast<int>(lanes.size());
     for (int i = 0; i < cap && i < *n; ++i) out[i] = lanes[i];
     return BLBRS_OK;
+}
+
+int blbrs_encoder_lane_stats(blbrs_encoder* enc, int lane, blbrs_lane_stats* out) {
+    if (!enc || !out || lane < 0) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
+    std::vector<int> lanes;
+    int rc = enc->lanes(&lanes);
+    if (rc) return rc;
+    if (static_cast<size_t>(lane) >= lanes.size()) return fail(BLBRS_ERR_INVALID_ARG, "lane out of range");
+    const auto key = rt::lane_keys(lanes)[lane];
+    return rt::lane_stats(key.first, key.second, out);
 }
 
 int blbrs_set_default_devices(const int* devices, int ndevices) {
@@ -1228,21 +1290,22 @@ int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size
     // Contiguous split of the stripes over the device list (multigpu.stripe_range's rule).
     const size_t parts = std::min(lanes.size(), batch);
     struct Part {
-        int dev;
+        int dev, occ;
         size_t start, count;
         int rc = BLBRS_OK;
         std::string msg;
     };
     std::vector<Part> ps;
+    const auto keys = rt::lane_keys(lanes);
     const size_t base = batch / parts, extra = batch % parts;
     for (size_t p = 0, start = 0; p < parts; ++p) {
         const size_t count = base + (p < extra ? 1 : 0);
-        ps.push_back(Part{lanes[p], start, count});
+        ps.push_back(Part{lanes[p], keys[p].second, start, count});
         start += count;
     }
     auto run_part = [&](Part& p) {
         rt::LoadTicket ticket;
-        ticket.take(p.dev);
+        ticket.take(p.dev, p.occ, static_cast<uint64_t>(p.count) * n * shard_len);
         rt::DeviceGuard guard;
         p.rc = guard.enter(p.dev);
         if (p.rc == BLBRS_OK) p.rc = host_run(enc, steps, shard_ptrs + p.start * n, p.count, shard_len, nullptr, p.dev);
@@ -1384,27 +1447,46 @@ int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {
     const bool visible = rt::device_view(data, &view, &owner);
     const int dev = owner >= 0 ? owner : lanes[rt::pick_lane(lanes, rr)];
     rt::LoadTicket ticket;
-    ticket.take(dev);
+    ticket.take(dev, 0, len);
     rt::DeviceGuard guard;
     if ((rc = guard.enter(dev))) return rc;
     rt::WorkerLease w;
     if ((rc = w.acquire(dev))) return rc;
     rt::note_call(dev);
     const size_t nblocks = (len + block - 1) / block;
-    const uint8_t* src = nullptr;
+    const hipStream_t s = w->s[0];
+    uint32_t* dout = nullptr;  // nblocks entries + one seed word
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dout), (nblocks + 1) * 4, s));
+    hipError_t e = hipSuccess;
     if (visible) {
-        src = reinterpret_cast<const uint8_t*>(view);  // pinned / device memory: in place
+        // Pinned / device memory: in place.
+        e = crc32c_blocks(reinterpret_cast<const uint8_t*>(view), len, 1, len, block, 0, nullptr, dout, s);
     } else {
-        if ((rc = w->ensure_stage(round_up(len, 256)))) return rc;
-        HIP_TRY(hipMemcpyAsync(w->stage, data, len, hipMemcpyHostToDevice, w->s[0]));
-        src = w->stage;
+        // Pageable: chunks of at most one ring slot through the worker's staging (the bound of
+        // blb_rs.h's worker limits, whatever len is).  With block <= the slot a chunk is whole
+        // blocks; a longer block (a whole bulk frame) is continued across chunks: the chunk at
+        // offset `off` starts (off mod block) bytes into block off / block, whose CRC so far is
+        // the seed (crc32.Update) and which the chunk's first entry overwrites.
+        const size_t slot = rt::kStageSlotBudget;
+        const size_t C = block <= slot ? slot / block * block : slot;
+        if ((rc = w->ensure_stage(round_up(std::min(C, len), 256)))) {
+            (void)hipFreeAsync(dout, s);
+            (void)hipStreamSynchronize(s);
+            return rc;
+        }
+        uint32_t* seed = dout + nblocks;
+        for (size_t off = 0; off < len && e == hipSuccess; off += C) {
+            const size_t clen = std::min(C, len - off), phase = off % block, first = off / block;
+            e = hipMemcpyAsync(w->stage, data + off, clen, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess && phase)
+                e = hipMemcpyAsync(seed, dout + first, 4, hipMemcpyDeviceToDevice, s);
+            if (e == hipSuccess)
+                e = crc32c_blocks(w->stage, clen, 1, clen, block, phase, phase ? seed : nullptr, dout + first, s);
+        }
     }
-    uint32_t* dout = nullptr;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dout), nblocks * 4, w->s[0]));
-    hipError_t e = crc32c_blocks(src, len, 1, len, block, 0, nullptr, dout, w->s[0]);
-    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, nblocks * 4, hipMemcpyDeviceToHost, w->s[0]);
-    (void)hipFreeAsync(dout, w->s[0]);
-    const hipError_t f = hipStreamSynchronize(w->s[0]);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, nblocks * 4, hipMemcpyDeviceToHost, s);
+    (void)hipFreeAsync(dout, s);
+    const hipError_t f = hipStreamSynchronize(s);
     if (e == hipSuccess) e = f;
     if (e != hipSuccess) return hip_fail(e, "crc32c");
     return BLBRS_OK;
@@ -1582,6 +1664,12 @@ int blbrs_buffer_get(size_t n, uint8_t** out, size_t* cap) {
 
 int blbrs_buffer_put(uint8_t* p) { return rt::pool_put(p); }
 
+int blbrs_buffer_register(void* p, size_t n) { return rt::pool_register(p, n); }
+
+int blbrs_buffer_unregister(void* p) { return rt::pool_unregister(p); }
+
+int blbrs_pool_set_live_limit(size_t bytes) { return rt::pool_set_live_limit(bytes); }
+
 int blbrs_pool_set_idle_limit(size_t bytes) { return rt::pool_set_idle_limit(bytes); }
 
 int blbrs_get_pool_stats(blbrs_pool_stats* out) {
@@ -1666,6 +1754,7 @@ const char* blbrs_strerror(int code) {
         case BLBRS_ERR_INVALID_ARG: return "invalid argument";
         case BLBRS_ERR_HIP: return "HIP runtime error";
         case BLBRS_ERR_NO_DEVICE: return "no HIP device";
+        case BLBRS_ERR_LIMIT: return "pinned-memory live limit reached";
         default: return "unknown error";
     }
 }

@@ -31,6 +31,7 @@
 //    combine shifts back out like any block end inside a tile.
 #include "encode_crc.hpp"
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 
@@ -86,6 +87,19 @@ struct TileConsts {
 #define BLBRS_ECT_TABSEQ 1
 #endif
 constexpr int kTabSeq = BLBRS_ECT_TABSEQ;
+
+// 1 = the split wave's second pass zeroes the acc dwords before the boundary in place, so the
+// chain loop carries no per-dword masks (A/B builds).
+#ifndef BLBRS_ECT_MASKACC
+#define BLBRS_ECT_MASKACC 0
+#endif
+constexpr int kMaskAcc = BLBRS_ECT_MASKACC;
+// N > 0 = persistent grid of N workgroups per CU, each walking its XCD's tiles in a loop with
+// the constants staged once (A/B builds).
+#ifndef BLBRS_ECT_PERSIST
+#define BLBRS_ECT_PERSIST 0
+#endif
+[[maybe_unused]] constexpr int kPersist = BLBRS_ECT_PERSIST;
 
 struct TArgs {
     const uint32_t* tables;
@@ -198,10 +212,17 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
         uint32_t crc[MR];
 #pragma unroll
         for (int j = 0; j < MR; ++j) crc[j] = 0u;
+        if constexpr (kMaskAcc) {
+            if (pass == 1)
+#pragma unroll
+                for (int d = 0; d < NV; ++d)
+#pragma unroll
+                    for (int j = 0; j < MR; ++j) acc[j][d] = mine + 4u * d >= o ? acc[j][d] : 0u;
+        }
 #pragma unroll
         for (int d = 0; d < NV; d += 2) {
-            const bool keep0 = pass == 0 || mine + 4u * d >= o;
-            const bool keep1 = pass == 0 || mine + 4u * d + 4u >= o;
+            const bool keep0 = kMaskAcc || pass == 0 || mine + 4u * d >= o;
+            const bool keep1 = kMaskAcc || pass == 0 || mine + 4u * d + 4u >= o;
 #pragma unroll
             for (int j = 0; j < MR; ++j) {
                 const uint32_t x = crc[j] ^ (keep0 ? acc[j][d] : 0u), y = keep1 ? acc[j][d + 1] : 0u;
@@ -264,6 +285,59 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
     }
 }
 
+// All K inputs of the tile in flight (nontemporal: every byte is read once).
+template <int K, int LC, bool PARTIAL>
+__device__ __forceinline__ void load_tile(const TArgs& a, const uint8_t* stripe, uint64_t tile_off, uint32_t in_tile,
+                                          uint32_t lim, uint32_t (&x)[K][LC / 4]) {
+    constexpr int NQ = LC / 16;
+    const ci32 in_idx = as_const(a.in_idx);
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        const uint8_t* p = stripe + static_cast<uint64_t>(in_idx[c]) * a.shard_stride + tile_off + in_tile;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (!PARTIAL || in_tile + 1024u * q < lim)
+                v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q));
+            x[c][4 * q] = v.x;
+            x[c][4 * q + 1] = v.y;
+            x[c][4 * q + 2] = v.z;
+            x[c][4 * q + 3] = v.w;
+        }
+    }
+}
+
+// The parity rows of the tile (v_perm multiply), stored nontemporal; acc keeps them.
+template <int K, int MR, int LC, bool PARTIAL>
+__device__ __forceinline__ void code_tile(const TArgs& a, uint8_t* stripe, uint64_t tile_off, uint32_t in_tile,
+                                          uint32_t lim, uint32_t (&x)[K][LC / 4], uint32_t (&acc)[MR][LC / 4]) {
+    constexpr int NV = LC / 4;
+    constexpr int NQ = LC / 16;
+    const ci32 out_idx = as_const(a.out_idx);
+    {
+        cu32 tables = as_const(a.tables);
+        asm volatile("" : "+s"(tables));
+#pragma unroll
+        for (int c = 0; c + 1 < K; c += 2) {
+            if constexpr (kTabSeq > 0)
+                if (c >= 2 * kTabSeq) asm volatile("" : "+s"(tables) : "v"(acc[0][0]));
+            madd2<MR, NV>(Groups<NV>(x[c]), [&](int r) { return tables + (r * K + c) * 5; }, Groups<NV>(x[c + 1]),
+                          [&](int r) { return tables + (r * K + c + 1) * 5; }, acc, MR);
+        }
+        if constexpr (K & 1)
+            madd<MR, NV>(Groups<NV>(x[K - 1]), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, MR);
+    }
+#pragma unroll
+    for (int j = 0; j < MR; ++j) {
+        uint8_t* q = stripe + static_cast<uint64_t>(out_idx[j]) * a.shard_stride + tile_off + in_tile;
+#pragma unroll
+        for (int u = 0; u < NQ; ++u)
+            if (!PARTIAL || in_tile + 1024u * u < lim)
+                __builtin_nontemporal_store(u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
+                                            reinterpret_cast<u32x4*>(q + 1024 * u));
+    }
+}
+
 // One workgroup = one tile of one stripe (PARTIAL: the stripe's partial last tile, in a
 // second B-workgroup launch so that the masking never touches the main kernel).  Several
 // tiles per workgroup (constants staged once, the next tile's loads issued under this
@@ -271,7 +345,6 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
 template <int K, int MR, int LC, bool PARTIAL>
 __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     constexpr int NV = LC / 4;
-    constexpr int NQ = LC / 16;
     constexpr uint32_t kRow = 64u * LC;
     constexpr uint32_t kTile = 4u * kRow;
     __shared__ uint32_t tab[8 * 256];
@@ -296,8 +369,6 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     const uint32_t in_tile = wave * kRow + lane_piece<LC>(lane);  // tile offset of piece q = 0
     // Bytes of the partial tile inside the shard (a multiple of 16).
     const uint32_t lim = PARTIAL ? static_cast<uint32_t>(a.S - tile_off) : kTile;
-    const ci32 in_idx = as_const(a.in_idx);
-    const ci32 out_idx = as_const(a.out_idx);
 
     // Constants (L2 hits) into registers first, then the data loads: the LDS writes below
     // wait for the constants only (in-order vmcnt).
@@ -312,22 +383,8 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
         nv[r] = (kFlags & 1) ? tid * 5u + r : i < kNibWords ? a.nib[i] : 0u;
     }
     const uint32_t wmv = tid < 96u ? a.wavemat[tid] : 0u;
-    // All K inputs of the tile in flight (nontemporal: every byte is read once).
     uint32_t x[K][NV];
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        const uint8_t* p = stripe + static_cast<uint64_t>(in_idx[c]) * a.shard_stride + tile_off + in_tile;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            u32x4 v = u32x4{0u, 0u, 0u, 0u};
-            if (!PARTIAL || in_tile + 1024u * q < lim)
-                v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q));
-            x[c][4 * q] = v.x;
-            x[c][4 * q + 1] = v.y;
-            x[c][4 * q + 2] = v.z;
-            x[c][4 * q + 3] = v.w;
-        }
-    }
+    load_tile<K, LC, PARTIAL>(a, stripe, tile_off, in_tile, lim, x);
 #pragma unroll
     for (int r = 0; r < kFill; ++r) tab[tid + r * kTThreads] = tv[r];
 #pragma unroll
@@ -338,34 +395,59 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     if (tid < 96u) wm[tid] = wmv;
 
     uint32_t acc[MR][NV] = {};
-    {
-        cu32 tables = as_const(a.tables);
-        asm volatile("" : "+s"(tables));
-#pragma unroll
-        for (int c = 0; c + 1 < K; c += 2) {
-            if constexpr (kTabSeq > 0)
-                if (c >= 2 * kTabSeq) asm volatile("" : "+s"(tables) : "v"(acc[0][0]));
-            madd2<MR, NV>(Groups<NV>(x[c]), [&](int r) { return tables + (r * K + c) * 5; }, Groups<NV>(x[c + 1]),
-                          [&](int r) { return tables + (r * K + c + 1) * 5; }, acc, MR);
-        }
-        if constexpr (K & 1)
-            madd<MR, NV>(Groups<NV>(x[K - 1]), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, MR);
-    }
-#pragma unroll
-    for (int j = 0; j < MR; ++j) {
-        uint8_t* q = stripe + static_cast<uint64_t>(out_idx[j]) * a.shard_stride + tile_off + in_tile;
-#pragma unroll
-        for (int u = 0; u < NQ; ++u)
-            if (!PARTIAL || in_tile + 1024u * u < lim)
-                __builtin_nontemporal_store(u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
-                                            reinterpret_cast<u32x4*>(q + 1024 * u));
-    }
+    code_tile<K, MR, LC, PARTIAL>(a, stripe, tile_off, in_tile, lim, x, acc);
     // CRC of this lane's LC contiguous parity bytes (tile offset LC * tid) per row.
 #pragma unroll
     for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
     __syncthreads();  // tables
     crc_tile<MR, LC>(a, acc, tab, nib, wm, red, tile_off, static_cast<uint64_t>(b) * a.tps + tile, tid, lane, wave);
 }
+
+#if BLBRS_ECT_PERSIST
+// Persistent form (BLBRS_ECT_PERSIST workgroups per CU): constants staged once per workgroup,
+// then the workgroup walks tiles of its XCD's contiguous share in a loop.  The reduction
+// buffer alternates between two halves: crc_tile's barrier keeps the waves within one tile
+// of each other, so a wave writing tile i+1's row totals never meets the fold of tile i-1.
+template <int K, int MR, int LC>
+__global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu(kPersist > 3 ? kPersist : 3)))
+void encode_crc_tile_persist_kernel(TArgs a) {
+    constexpr int NV = LC / 4;
+    constexpr uint32_t kRow = 64u * LC;
+    constexpr uint32_t kTile = 4u * kRow;
+    __shared__ uint32_t tab[8 * 256];
+    __shared__ uint32_t nib[kNibWords];
+    __shared__ uint32_t red[2][2][4][MR];
+    __shared__ uint32_t wm[96];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (uint32_t i = tid; i < 8u * 256u; i += kTThreads) tab[i] = a.tab8[i];
+    for (uint32_t i = tid; i < kNibWords; i += kTThreads) nib[i] = a.nib[i];
+    if (tid < 96u) wm[tid] = a.wavemat[tid];
+    __syncthreads();
+    const uint32_t groups = a.B * a.tps_full;
+    // XCD x = blockIdx % 8 takes tiles [x * groups / 8, (x + 1) * groups / 8); its workgroups
+    // interleave over that range in dispatch order.
+    const uint32_t xcd = blockIdx.x % 8u, per_xcd = gridDim.x / 8u, local = blockIdx.x / 8u;
+    const uint32_t t0 = static_cast<uint32_t>(static_cast<uint64_t>(groups) * xcd / 8u);
+    const uint32_t t1 = static_cast<uint32_t>(static_cast<uint64_t>(groups) * (xcd + 1u) / 8u);
+    const uint32_t in_tile = wave * kRow + lane_piece<LC>(lane);
+    uint32_t it = 0;
+#pragma unroll 1
+    for (uint32_t t = t0 + local; t < t1; t += per_xcd, ++it) {
+        const uint32_t b = t / a.tps_full, tile = t - b * a.tps_full;
+        const uint64_t tile_off = static_cast<uint64_t>(tile) * kTile;
+        uint8_t* stripe = a.base + static_cast<uint64_t>(b) * a.stripe_stride;
+        uint32_t x[K][NV];
+        load_tile<K, LC, false>(a, stripe, tile_off, in_tile, kTile, x);
+        uint32_t acc[MR][NV] = {};
+        code_tile<K, MR, LC, false>(a, stripe, tile_off, in_tile, kTile, x, acc);
+#pragma unroll
+        for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
+        crc_tile<MR, LC>(a, acc, tab, nib, wm, red[it & 1u], tile_off, static_cast<uint64_t>(b) * a.tps + tile, tid,
+                         lane, wave);
+    }
+}
+#endif
 
 __device__ uint32_t shift_n(const CrcConsts* c, uint32_t r, uint64_t n) {
     const cu32 p = as_const(&c->pow2[0][0]);
@@ -477,6 +559,32 @@ KernelFn pick(int k, int rows, bool partial = false) {
         default: return nullptr;
     }
 }
+
+#if BLBRS_ECT_PERSIST
+template <int K>
+KernelFn pick_persist_rows(int rows) {
+    switch (rows) {
+        case 1: return encode_crc_tile_persist_kernel<K, 1, lc_for(K, 1)>;
+        case 2: return encode_crc_tile_persist_kernel<K, 2, lc_for(K, 2)>;
+        case 3: return encode_crc_tile_persist_kernel<K, 3, lc_for(K, 3)>;
+        case 4: return encode_crc_tile_persist_kernel<K, 4, lc_for(K, 4)>;
+        case 5: return encode_crc_tile_persist_kernel<K, 5, lc_for(K, 5)>;
+        default: return nullptr;
+    }
+}
+
+KernelFn pick_persist(int k, int rows) {
+    switch (k) {
+        case 3: return pick_persist_rows<3>(rows);
+        case 4: return pick_persist_rows<4>(rows);
+        case 6: return pick_persist_rows<6>(rows);
+        case 8: return pick_persist_rows<8>(rows);
+        case 10: return pick_persist_rows<10>(rows);
+        case 12: return pick_persist_rows<12>(rows);
+        default: return nullptr;
+    }
+}
+#endif
 
 std::mutex g_mu;
 std::map<int, const TileConsts*> g_consts;  // per device, process lifetime
@@ -592,7 +700,19 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     if ((e = hipMallocAsync(reinterpret_cast<void**>(&buf), nraw * 8, stream)) != hipSuccess) return e;
     a.raw = buf;
     a.hi = buf + nraw;
+#if BLBRS_ECT_PERSIST
+    if constexpr (kPersist > 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint64_t grid = std::min<uint64_t>(groups, static_cast<uint64_t>(cus) * kPersist) / 8u * 8u;
+        if (groups && grid >= 8)
+            hipLaunchKernelGGL(pick_persist(in.k, in.rows), dim3(static_cast<unsigned>(grid)), dim3(kTThreads), 0, stream, a);
+        else if (groups)
+            hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), 0, stream, a);
+    }
+#else
     if (groups) hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), 0, stream, a);
+#endif
     e = hipGetLastError();
     if (e == hipSuccess && a.tps != a.tps_full) {
         hipLaunchKernelGGL(pick(in.k, in.rows, true), dim3(in.B), dim3(kTThreads), 0, stream, a);

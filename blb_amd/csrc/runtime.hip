@@ -130,20 +130,82 @@ int64_t load_of(int dev) {
     return dev >= 0 && dev < kMaxDevices ? g_load[dev].load(std::memory_order_relaxed) : 0;
 }
 
+namespace {
+
+struct LaneLoad {
+    std::atomic<uint64_t> calls{0}, bytes{0};
+    std::atomic<int64_t> in_calls{0}, in_bytes{0};
+};
+LaneLoad g_lanes[kMaxDevices][kMaxLaneOcc];
+
+LaneLoad* lane_of(int dev, int occ) {
+    if (dev < 0 || dev >= kMaxDevices || occ < 0) return nullptr;
+    return &g_lanes[dev][std::min(occ, kMaxLaneOcc - 1)];
+}
+
+}  // namespace
+
+std::vector<std::pair<int, int>> lane_keys(const std::vector<int>& devs) {
+    std::vector<std::pair<int, int>> keys(devs.size());
+    for (size_t i = 0; i < devs.size(); ++i) {
+        int occ = 0;
+        for (size_t j = 0; j < i; ++j) occ += devs[j] == devs[i];
+        keys[i] = {devs[i], std::min(occ, kMaxLaneOcc - 1)};
+    }
+    return keys;
+}
+
 size_t pick_lane(const std::vector<int>& lanes, std::atomic<unsigned>& rr) {
     const size_t n = lanes.size();
+    const auto keys = lane_keys(lanes);
+    auto in_bytes = [&](size_t i) {
+        const LaneLoad* l = lane_of(keys[i].first, keys[i].second);
+        return l ? l->in_bytes.load(std::memory_order_relaxed) : 0;
+    };
     const size_t start = rr.fetch_add(1, std::memory_order_relaxed) % n;
     size_t best = start;
-    int64_t best_load = load_of(lanes[start]);
+    int64_t best_load = in_bytes(start);
     for (size_t j = 1; j < n && best_load > 0; ++j) {
         const size_t i = (start + j) % n;
-        const int64_t l = load_of(lanes[i]);
+        const int64_t l = in_bytes(i);
         if (l < best_load) {
             best = i;
             best_load = l;
         }
     }
     return best;
+}
+
+void LoadTicket::take(int d, int o, uint64_t b) {
+    dev = d;
+    occ = o;
+    bytes = b;
+    load_add(d, 1);
+    if (LaneLoad* l = lane_of(d, o)) {
+        l->calls.fetch_add(1, std::memory_order_relaxed);
+        l->bytes.fetch_add(b, std::memory_order_relaxed);
+        l->in_calls.fetch_add(1, std::memory_order_relaxed);
+        l->in_bytes.fetch_add(static_cast<int64_t>(b), std::memory_order_relaxed);
+    }
+}
+
+LoadTicket::~LoadTicket() {
+    if (dev < 0) return;
+    load_add(dev, -1);
+    if (LaneLoad* l = lane_of(dev, occ)) {
+        l->in_calls.fetch_sub(1, std::memory_order_relaxed);
+        l->in_bytes.fetch_sub(static_cast<int64_t>(bytes), std::memory_order_relaxed);
+    }
+}
+
+int lane_stats(int dev, int occ, blbrs_lane_stats* out) {
+    const LaneLoad* l = lane_of(dev, occ);
+    if (!l) return fail(BLBRS_ERR_INVALID_ARG, "no such lane");
+    out->calls = l->calls.load();
+    out->bytes = l->bytes.load();
+    out->inflight_calls = l->in_calls.load();
+    out->inflight_bytes = l->in_bytes.load();
+    return BLBRS_OK;
 }
 
 bool device_view(const void* p, uint64_t* view, int* owner) {
@@ -454,12 +516,21 @@ int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, con
 // ---------------------------------------------------------------------------------------
 //
 // Same capacity classes as blb's pool: 1 MiB, 4 MiB and 8 MiB (+ disk.ExtraRoom = one 64 KiB
-// ChecksumFile block, pkg/disk/checksum_file.go:27), plus a 128 KiB + ExtraRoom class for
-// the small buffers blb allocates with make() (pinning each of those separately would cost
-// more than the copy it saves).  Larger requests get an exact allocation, freed on Put.
-// Buffers are pinned and mapped for every device (hipHostMallocDefault = portable | mapped),
-// so the coding kernels read and write them in place over PCIe.  Like sync.Pool, Get never
-// blocks; idle buffers above the idle limit are freed on Put.
+// ChecksumFile block, pkg/disk/checksum_file.go:27), plus a 128 KiB + ExtraRoom class for the
+// library's own staging of small pageable shards (blb does not pool that size).  Larger
+// requests get an exact allocation, freed on Put.  Buffers are pinned and mapped for every
+// device (hipHostMallocDefault = portable | mapped), so the coding kernels read and write them
+// in place over PCIe.  Like sync.Pool, Get never blocks; idle buffers above the idle limit are
+// freed on Put.
+//
+// Lifetime.  blb's pool is a sync.Pool (pkg/rpc/pool.go:22-26): a buffer that is never
+// PutBuffer'd is simply garbage-collected, and blb relies on that (reconstruct.go:126-152
+// drops errored and straggling replies; bulk_codec.go:212-221 returns on a read error with
+// the buffer it took).  Library-owned buffers cannot follow the GC, so callers with that
+// pattern register memory they own instead (pool_register: the Go shim registers Go-heap
+// buffers and unregisters them from a finalizer), and every pinned byte -- handed out or
+// registered -- counts against a live limit: past it the pool refuses (BLBRS_ERR_LIMIT) and
+// the caller uses pageable memory, which the engine stages.
 
 namespace {
 
@@ -471,10 +542,17 @@ constexpr int kNumClasses = 4;
 struct HostPool {
     std::mutex mu;
     std::vector<uint8_t*> free_list[kNumClasses];
-    std::unordered_map<uint8_t*, size_t> live;  // every buffer handed out -> capacity
-    size_t idle_bytes = 0, live_bytes = 0;
+    std::unordered_map<uint8_t*, size_t> live;        // every buffer handed out -> capacity
+    std::unordered_map<uintptr_t, size_t> registered;  // caller memory pinned -> length
+    size_t idle_bytes = 0, live_bytes = 0, registered_bytes = 0;
     size_t idle_limit = size_t{4} << 30;
-    uint64_t gets = 0, puts = 0, allocs = 0, frees = 0;
+    size_t live_limit = size_t{16} << 30;  // 0 = none
+    uint64_t gets = 0, puts = 0, allocs = 0, frees = 0, registrations = 0, rejects = 0;
+
+    // Room for `bytes` more pinned bytes under the live limit (mu held).
+    bool room_for(size_t bytes) const {
+        return live_limit == 0 || live_bytes + registered_bytes + bytes <= live_limit;
+    }
 };
 
 HostPool& host_pool() {
@@ -488,9 +566,15 @@ int class_of(size_t cap) {
     return -1;
 }
 
+int limit_fail(HostPool& p, size_t want) {
+    ++p.rejects;
+    return fail(BLBRS_ERR_LIMIT, "pinned live limit reached (" + std::to_string(p.live_bytes + p.registered_bytes) +
+                                     " + " + std::to_string(want) + " > " + std::to_string(p.live_limit) + " bytes)");
+}
+
 }  // namespace
 
-int pool_get(size_t n, uint8_t** out, size_t* cap) {
+int pool_get(size_t n, uint8_t** out, size_t* cap, bool internal) {
     *out = nullptr;
     if (n == 0) return fail(BLBRS_ERR_INVALID_ARG, "zero-length buffer");
     HostPool& p = host_pool();
@@ -501,6 +585,7 @@ int pool_get(size_t n, uint8_t** out, size_t* cap) {
     {
         std::lock_guard<std::mutex> g(p.mu);
         ++p.gets;
+        if (!internal && !p.room_for(want)) return limit_fail(p, want);
         if (c < kNumClasses && !p.free_list[c].empty()) {
             uint8_t* b = p.free_list[c].back();
             p.free_list[c].pop_back();
@@ -511,16 +596,22 @@ int pool_get(size_t n, uint8_t** out, size_t* cap) {
             *cap = want;
             return BLBRS_OK;
         }
+        // Reserve the bytes before allocating outside the lock, so that concurrent gets
+        // cannot overshoot the limit together.
+        p.live_bytes += want;
     }
     int nd = 0;
     int rc = device_count(&nd);
-    if (rc) return rc;
     uint8_t* b = nullptr;
-    BLBRS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&b), want, hipHostMallocDefault));
+    hipError_t e = hipSuccess;
+    if (rc == BLBRS_OK) e = hipHostMalloc(reinterpret_cast<void**>(&b), want, hipHostMallocDefault);
     std::lock_guard<std::mutex> g(p.mu);
+    if (rc != BLBRS_OK || e != hipSuccess) {
+        p.live_bytes -= want;
+        return rc != BLBRS_OK ? rc : hip_fail(e, "hipHostMalloc");
+    }
     ++p.allocs;
     p.live[b] = want;
-    p.live_bytes += want;
     *out = b;
     *cap = want;
     return BLBRS_OK;
@@ -551,6 +642,49 @@ int pool_put(uint8_t* b) {
     return BLBRS_OK;
 }
 
+int pool_register(void* ptr, size_t n) {
+    if (!ptr || n == 0) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument or zero length");
+    HostPool& p = host_pool();
+    const uintptr_t key = reinterpret_cast<uintptr_t>(ptr);
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        if (p.registered.count(key)) return fail(BLBRS_ERR_INVALID_ARG, "memory is already registered");
+        if (!p.room_for(n)) return limit_fail(p, n);
+        p.registered[key] = n;  // reserved; undone below if pinning fails
+        p.registered_bytes += n;
+    }
+    int nd = 0;
+    int rc = device_count(&nd);
+    hipError_t e = hipSuccess;
+    if (rc == BLBRS_OK) e = hipHostRegister(ptr, n, hipHostRegisterPortable | hipHostRegisterMapped);
+    std::lock_guard<std::mutex> g(p.mu);
+    if (rc != BLBRS_OK || e != hipSuccess) {
+        p.registered.erase(key);
+        p.registered_bytes -= n;
+        if (e != hipSuccess) (void)hipGetLastError();
+        return rc != BLBRS_OK ? rc : hip_fail(e, "hipHostRegister");
+    }
+    ++p.registrations;
+    return BLBRS_OK;
+}
+
+int pool_unregister(void* ptr) {
+    if (!ptr) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    HostPool& p = host_pool();
+    const uintptr_t key = reinterpret_cast<uintptr_t>(ptr);
+    size_t n = 0;
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        auto it = p.registered.find(key);
+        if (it == p.registered.end()) return fail(BLBRS_ERR_INVALID_ARG, "memory was not registered by blbrs_buffer_register");
+        n = it->second;
+        p.registered.erase(it);
+        p.registered_bytes -= n;
+    }
+    BLBRS_HIP_TRY(hipHostUnregister(ptr));
+    return BLBRS_OK;
+}
+
 int pool_set_idle_limit(size_t bytes) {
     HostPool& p = host_pool();
     {
@@ -558,6 +692,13 @@ int pool_set_idle_limit(size_t bytes) {
         p.idle_limit = bytes;
     }
     if (bytes == 0) pool_trim();
+    return BLBRS_OK;
+}
+
+int pool_set_live_limit(size_t bytes) {
+    HostPool& p = host_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    p.live_limit = bytes;
     return BLBRS_OK;
 }
 
@@ -570,6 +711,10 @@ int pool_stats(blbrs_pool_stats* out) {
     out->frees = p.frees;
     out->live_bytes = p.live_bytes;
     out->idle_bytes = p.idle_bytes;
+    out->registered_bytes = p.registered_bytes;
+    out->registrations = p.registrations;
+    out->live_limit = p.live_limit;
+    out->limit_rejects = p.rejects;
     return BLBRS_OK;
 }
 

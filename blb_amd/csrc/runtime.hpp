@@ -66,18 +66,26 @@ class DeviceGuard {
     int prev_ = -1;
 };
 
-// Calls in flight per device (host-memory calls and batch parts), for least-loaded choice.
+// Load accounting.  A device list may repeat a device: entry i is lane (dev, occ) where occ
+// counts the earlier entries naming the same device, so [0, 0] is two lanes on GPU 0 and an
+// encoder on [0, 1] shares lane (0, 0) with every other list that names GPU 0 once.  Each lane
+// counts calls and bytes (cumulative and in flight); each device counts calls in flight.
+constexpr int kMaxLaneOcc = 16;
 void load_add(int dev, int delta);
 int64_t load_of(int dev);
-// Index into `lanes` of the least-loaded entry; ties rotate through `rr`.
+// (dev, occ) of every entry of a device list.
+std::vector<std::pair<int, int>> lane_keys(const std::vector<int>& devs);
+// Index into `lanes` of the entry with the fewest BYTES in flight (a 4 KiB degraded read and
+// an 8 MiB increment do not weigh the same); ties rotate through `rr`.
 size_t pick_lane(const std::vector<int>& lanes, std::atomic<unsigned>& rr);
+int lane_stats(int dev, int occ, blbrs_lane_stats* out);
 
+// Holds one call's load on a lane (and its device) for the call's duration.
 struct LoadTicket {
-    int dev = -1;
-    void take(int d) { dev = d; load_add(d, 1); }
-    ~LoadTicket() {
-        if (dev >= 0) load_add(dev, -1);
-    }
+    int dev = -1, occ = 0;
+    uint64_t bytes = 0;
+    void take(int d, int o = 0, uint64_t b = 0);
+    ~LoadTicket();
 };
 
 // Address under which the GPU reaches `p`: device memory as is, pinned host memory
@@ -146,9 +154,16 @@ class PtrLease {
 };
 
 // ---- pinned buffer pool (rpc.GetBuffer / PutBuffer over pinned, device-mapped memory) ----
-int pool_get(size_t n, uint8_t** out, size_t* cap);
+// Every pinned byte the pool hands out or registers counts against the live limit; past it
+// pool_get / pool_register fail with BLBRS_ERR_LIMIT and callers fall back to pageable
+// memory.  `internal` = the library's own transient staging (bounded by the calls in
+// flight), which is counted but never refused.
+int pool_get(size_t n, uint8_t** out, size_t* cap, bool internal = false);
 int pool_put(uint8_t* p);
+int pool_register(void* p, size_t n);
+int pool_unregister(void* p);
 int pool_set_idle_limit(size_t bytes);
+int pool_set_live_limit(size_t bytes);
 int pool_stats(blbrs_pool_stats* out);
 void pool_trim();
 

@@ -71,8 +71,13 @@ class ErrNoDevice(RSError):
     code = -9
 
 
+class ErrLimit(RSError):
+    """The pinned-memory live limit is reached (blbrs_pool_set_live_limit): use pageable memory."""
+    code = -10
+
+
 _ERRORS = {c.code: c for c in (ErrInvShardNum, ErrMaxShardNum, ErrTooFewShards, ErrShardNoData,
-                                ErrShardSize, ErrSingular, ErrInvalidArgument, ErrHIP, ErrNoDevice)}
+                                ErrShardSize, ErrSingular, ErrInvalidArgument, ErrHIP, ErrNoDevice, ErrLimit)}
 
 
 def _check(rc: int) -> None:
@@ -147,6 +152,13 @@ class Encoder:
         out = (ctypes.c_int * max(1, n.value))()
         _check(self._lib.blbrs_encoder_devices(self._h, out, n.value, ctypes.byref(n)))
         return list(out[:n.value])
+
+    def LaneStats(self, lane: int) -> dict:
+        """Load of entry `lane` of the device list: calls / shard bytes routed to it so far and
+        in flight now (blbrs_encoder_lane_stats)."""
+        st = _lib.LaneStats()
+        _check(self._lib.blbrs_encoder_lane_stats(self._h, int(lane), ctypes.byref(st)))
+        return {f: int(getattr(st, f)) for f, _ in st._fields_}
 
     def matrix(self) -> np.ndarray:
         out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
@@ -496,6 +508,12 @@ def GetBuffer(n: int) -> np.ndarray:
 
 def PutBuffer(buf: np.ndarray) -> None:
     _check(_lib.load().blbrs_buffer_put(buf.__array_interface__["data"][0]))
+
+
+def set_live_limit(nbytes: int) -> None:
+    """Cap on pinned bytes alive at once: buffers handed out by GetBuffer plus memory
+    registered by rpc.GetBuffer's pools (0 = no cap; default 16 GiB)."""
+    _check(_lib.load().blbrs_pool_set_live_limit(int(nbytes)))
 
 
 def pool_stats() -> dict:

@@ -14,6 +14,8 @@
 //	pkg/rpc/pool.go:30   GetBuffer(n)            ->  rsgpu.GetBuffer(n)
 //	pkg/rpc/pool.go:51   PutBuffer(b, exclusive) ->  rsgpu.PutBuffer(b, exclusive)
 //
+// (the pool keeps pool.go's Go-heap buffers and GC lifetime; it only pins them -- see below)
+//
 // Every encoder spreads its calls over all visible GPUs (the library picks the least-loaded
 // device per call; no goroutine or OS thread carries device state).  NewOn binds an encoder
 // to an explicit device list.
@@ -114,33 +116,104 @@ func SetWorkerLimit(perDevice int) error {
 }
 
 // ---- pinned buffer pool: pkg/rpc/pool.go's GetBuffer / PutBuffer ----
+//
+// blb's pool is three sync.Pools of Go-heap buffers, and blb relies on the GC for buffers it
+// never puts back: client/blb/reconstruct.go:126-152 puts back only the first n good replies
+// (errored and straggling ones are dropped after cancel()), bulk_codec.go:212-221 returns on
+// a read error with the buffer it took.  So this pool hands out Go memory, exactly as
+// pool.go does, and pins the buffers its pools create: a new class buffer is registered with
+// the engine (blbrs_buffer_register: pinned, mapped for every GPU, so Encode / Reconstruct*
+// code shards on it in place) and carries a finalizer on its backing array that unregisters
+// it before the GC frees it.  A dropped buffer is therefore unpinned when it is collected,
+// and the pinned bytes alive at once are capped by the engine's live limit
+// (SetPinnedLimit): past it registration is refused and the buffer stays pageable -- correct,
+// only staged by the engine -- and is registered again when the pool hands it out later.
+// Small (<= 128 KiB + ExtraRoom) and large (> the 8 MiB class) requests get make(), as in
+// pool.go.  The engine keeps the registered address only while the buffer is alive, and only
+// coding calls (during which the caller holds the slice) touch the memory.
 
-// GetBuffer returns a []byte with length n and capacity >= n (blb's pool classes: 1, 4 and
-// 8 MiB + disk.ExtraRoom) in pinned host memory mapped for every GPU.  The buffer may not be
-// zeroed!  The memory is C memory: cgo calls may pass it freely, and shards built on it are
-// coded in place (zero-copy) by Encode / Reconstruct*.  It falls back to make() when no GPU
-// is usable, so callers never see an error.
-func GetBuffer(n int) []byte {
-	if n <= 0 {
-		return make([]byte, n)
+const (
+	extraRoom  = 64 << 10 // disk.ExtraRoom
+	smallMax   = 128<<10 + extraRoom
+	buf1MBSize = 1<<20 + extraRoom
+	buf4MBSize = 4<<20 + extraRoom
+	buf8MBSize = 8<<20 + extraRoom
+)
+
+var (
+	buf8MBPool = sync.Pool{New: func() interface{} { return newPinned(buf8MBSize) }}
+	buf4MBPool = sync.Pool{New: func() interface{} { return newPinned(buf4MBSize) }}
+	buf1MBPool = sync.Pool{New: func() interface{} { return newPinned(buf1MBSize) }}
+	// Base addresses of the class buffers currently registered with the engine.
+	pinned sync.Map // uintptr -> struct{}
+)
+
+// register pins b's backing array with the engine and arranges for it to be unpinned when the
+// GC collects it.  b must be a whole class buffer (b[0] is the start of its allocation).
+func register(b []byte) {
+	p := &b[0]
+	addr := uintptr(unsafe.Pointer(p))
+	if C.blbrs_buffer_register(unsafe.Pointer(p), C.size_t(len(b))) != C.BLBRS_OK {
+		return // live limit reached (or no GPU): the buffer stays pageable
 	}
-	var p *C.uint8_t
-	var capacity C.size_t
-	if C.blbrs_buffer_get(C.size_t(n), &p, &capacity) != C.BLBRS_OK {
-		return make([]byte, n)
-	}
-	return unsafe.Slice((*byte)(unsafe.Pointer(p)), int(capacity))[:n]
+	pinned.Store(addr, struct{}{})
+	runtime.SetFinalizer(p, func(p *byte) {
+		pinned.Delete(uintptr(unsafe.Pointer(p)))
+		C.blbrs_buffer_unregister(unsafe.Pointer(p))
+	})
 }
 
-// PutBuffer returns a buffer to the pool.  As in pkg/rpc/pool.go it is fine to call on any
-// buffer that is not used again; non-exclusive or Go-allocated buffers are left alone.
+func newPinned(size int) interface{} {
+	b := make([]byte, size)
+	register(b)
+	return &b
+}
+
+func getClass(pool *sync.Pool, n int) []byte {
+	b := *pool.Get().(*[]byte)
+	b = b[:cap(b)] // a put slice may be shorter; its cap is the class size
+	if _, ok := pinned.Load(uintptr(unsafe.Pointer(&b[0]))); !ok {
+		register(b) // refused earlier: try again now that it is reused
+	}
+	return b[:n]
+}
+
+// GetBuffer returns a []byte with length n and capacity >= n.  The buffer may not be zeroed!
+// (pkg/rpc/pool.go:28-43.)  Buffers of the 1, 4 and 8 MiB classes are pinned while the live
+// limit allows.
+func GetBuffer(n int) []byte {
+	if n <= smallMax {
+		return make([]byte, n)
+	} else if n <= buf1MBSize {
+		return getClass(&buf1MBPool, n)
+	} else if n <= buf4MBSize {
+		return getClass(&buf4MBPool, n)
+	} else if n <= buf8MBSize {
+		return getClass(&buf8MBPool, n)
+	}
+	return make([]byte, n)
+}
+
+// PutBuffer returns a buffer to the pool (pkg/rpc/pool.go:45-62).  It is fine to call on any
+// buffer that is not used again, and fine not to call at all: the GC unpins what it collects.
 func PutBuffer(b []byte, exclusive bool) {
-	if !exclusive || cap(b) == 0 {
+	if !exclusive {
 		return
 	}
-	// blbrs_buffer_put ignores (INVALID_ARG) pointers it did not hand out, such as the
-	// make() fallback above.
-	C.blbrs_buffer_put((*C.uint8_t)(unsafe.Pointer(&b[:1][0])))
+	switch cap(b) {
+	case buf8MBSize:
+		buf8MBPool.Put(&b)
+	case buf4MBSize:
+		buf4MBPool.Put(&b)
+	case buf1MBSize:
+		buf1MBPool.Put(&b)
+	}
+}
+
+// SetPinnedLimit caps the bytes pinned at once (blbrs_pool_set_live_limit; default 16 GiB,
+// 0 = no cap).  Buffers the pool creates beyond it are plain Go memory.
+func SetPinnedLimit(bytes int64) error {
+	return call(func() C.int { return C.blbrs_pool_set_live_limit(C.size_t(bytes)) })
 }
 
 // ChecksumBlocks returns crc32.Checksum(block, castagnoliTable) for every `block`-byte block

@@ -54,6 +54,8 @@ extern "C" {
 #define BLBRS_ERR_INVALID_ARG   (-7) /* NULL pointer / bad stride / missing output buffer */
 #define BLBRS_ERR_HIP           (-8) /* HIP runtime failure; see blbrs_last_error() */
 #define BLBRS_ERR_NO_DEVICE     (-9) /* no gfx950 device visible */
+#define BLBRS_ERR_LIMIT        (-10) /* pinned-memory live limit reached (blbrs_pool_set_live_limit):
+                                        the caller falls back to pageable memory */
 
 typedef struct blbrs_encoder blbrs_encoder;
 typedef struct blbrs_batcher blbrs_batcher;
@@ -74,7 +76,20 @@ typedef struct {
     uint64_t allocs, frees;  /* pinned allocations made / released */
     uint64_t live_bytes;     /* capacity handed out and not yet put back */
     uint64_t idle_bytes;     /* capacity kept for reuse */
+    uint64_t registered_bytes; /* caller memory pinned by blbrs_buffer_register, not yet unregistered */
+    uint64_t registrations;  /* blbrs_buffer_register calls that pinned memory */
+    uint64_t live_limit;     /* cap on live_bytes + registered_bytes (blbrs_pool_set_live_limit) */
+    uint64_t limit_rejects;  /* gets / registrations refused with BLBRS_ERR_LIMIT */
 } blbrs_pool_stats;
+
+/* Load of one lane (blbrs_encoder_lane_stats): entry i of an encoder's device list.  A
+ * repeated device id is a further lane on that device ([0, 0] = two lanes on GPU 0). */
+typedef struct {
+    uint64_t calls;          /* host calls routed to the lane so far */
+    uint64_t bytes;          /* their shard bytes (k+m shards x length) */
+    int64_t inflight_calls;  /* of which running now */
+    int64_t inflight_bytes;
+} blbrs_lane_stats;
 
 /* One device's share of a device-resident batch (blbrs_*_parts). */
 typedef struct {
@@ -92,7 +107,8 @@ typedef struct {
  * k <= 0 or m <= 0, MAX_SHARD_NUM when k + m > 256. */
 int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out);
 /* reedsolomon.New on an explicit device list.  Host-memory calls of the encoder run on the
- * least-loaded entry; blbrs_encode_host_batch splits its stripes over the entries.  Entries
+ * entry with the fewest shard bytes in flight; blbrs_encode_host_batch splits its stripes over
+ * the entries.  Entries
  * may repeat ([0, 0] = two lanes on GPU 0).  blbrs_new(k, m) uses the process default list:
  * blbrs_set_default_devices(), else $BLBRS_DEVICES ("0,2,..."), else every visible device.
  * Device ids are checked at the first call that needs a device (INVALID_ARG / NO_DEVICE). */
@@ -100,6 +116,9 @@ int blbrs_new_on(int data_shards, int parity_shards, const int* devices, int nde
 /* The encoder's device list (the default list resolved): *n = its length, up to cap ids
  * copied to out. */
 int blbrs_encoder_devices(blbrs_encoder* enc, int* out, int cap, int* n);
+/* Load of entry `lane` of the encoder's device list (shared with every encoder whose list
+ * maps to the same (device, repeat) lane). */
+int blbrs_encoder_lane_stats(blbrs_encoder* enc, int lane, blbrs_lane_stats* out);
 /* Process default device list for blbrs_new encoders; (NULL, 0) = back to $BLBRS_DEVICES /
  * every visible device.  Encoders created earlier keep the list they resolved. */
 int blbrs_set_default_devices(const int* devices, int ndevices);
@@ -187,15 +206,35 @@ int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size
 
 /* ---- pinned host memory: rpc.GetBuffer / PutBuffer (pkg/rpc/pool.go:16-62) ----
  * blb's shards come from rpc.GetBuffer: pooled, NOT zeroed, capacity classes of 1, 4 and
- * 8 MiB + disk.ExtraRoom (64 KiB).  blbrs_buffer_get returns a buffer of the same class in
- * pinned memory mapped for every device, so host-memory calls on it run zero-copy (the
- * kernels read and write it over PCIe, no staging).  *cap is the class capacity (>= n).
- * Requests above the 8 MiB class get an exact allocation that blbrs_buffer_put frees.
- * Never blocks (like sync.Pool); idle buffers above the idle limit (default 4 GiB) are freed
- * on put.  put of a pointer not from get is INVALID_ARG. */
+ * 8 MiB + disk.ExtraRoom (64 KiB).  Pinned shards are coded zero-copy (the kernels read and
+ * write them over PCIe, no staging).  Two ways to get them:
+ *
+ * 1. Library-owned buffers (C / C++ callers with explicit or refcounted lifetime):
+ *    blbrs_buffer_get returns a buffer of blb's class in pinned memory mapped for every
+ *    device; *cap is the class capacity (>= n).  Besides blb's classes there is a 128 KiB +
+ *    ExtraRoom class, used by the library's own staging (blb does not pool that size, and
+ *    the Go shim returns make() for it).  Requests above the 8 MiB class get an exact
+ *    allocation that blbrs_buffer_put frees.  Never blocks (like sync.Pool); idle buffers
+ *    above the idle limit (default 4 GiB) are freed on put.  put of a pointer not from get is
+ *    INVALID_ARG.  A buffer that is never put stays allocated: callers whose buffers may be
+ *    dropped without a put (Go's rpc.GetBuffer users: bulk_codec.go:212-221 on a read error,
+ *    reconstruct.go:126-152 stragglers) must use (2).
+ * 2. Caller-owned memory (the Go shim: Go-heap buffers whose lifetime the GC decides):
+ *    blbrs_buffer_register pins [p, p+n) (portable, mapped) and blbrs_buffer_unregister
+ *    unpins it; the owner unregisters before the memory is freed (Go: a finalizer on the
+ *    backing array).  Nothing else is retained.
+ *
+ * Both count against the live limit (default 16 GiB, blbrs_pool_set_live_limit; 0 = no
+ * limit): live = capacity handed out and not put back + bytes registered.  A get or register
+ * that would exceed it fails with BLBRS_ERR_LIMIT and pins nothing -- the caller uses pageable
+ * memory instead (make()), which the engine stages.  The library's own transient staging is
+ * counted but never refused. */
 int blbrs_buffer_get(size_t n, uint8_t** out, size_t* cap);
 int blbrs_buffer_put(uint8_t* p);
+int blbrs_buffer_register(void* p, size_t n);
+int blbrs_buffer_unregister(void* p);
 int blbrs_pool_set_idle_limit(size_t bytes);
+int blbrs_pool_set_live_limit(size_t bytes);
 int blbrs_get_pool_stats(blbrs_pool_stats* out);
 /* Plain pinned allocations (hipHostMalloc, portable + mapped) and registration of existing
  * host memory (hipHostRegister, portable + mapped) for callers with their own pools. */
@@ -222,7 +261,10 @@ int blbrs_trim(void);
  * each buffer: for a buffer that starts inside a file block use blbrs_crc32c_dev_at. */
 int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block,
                      uint32_t* out_dev, void* stream);
-/* Host-memory form: one buffer; out (host) has ceil(len / block) entries. */
+/* Host-memory form: one buffer; out (host) has ceil(len / block) entries.  Pinned / device
+ * memory is read in place; pageable memory is staged in chunks of at most 16 MiB (block
+ * boundaries kept through the phase / seed continuation below), so a call's device staging
+ * stays within the worker bound whatever `len` is. */
 int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out);
 
 /* Encode fused with the CRC-32C of the parity it writes, in one pass over HBM: what

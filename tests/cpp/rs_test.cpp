@@ -25,6 +25,7 @@
 #include <thread>
 #include <vector>
 
+#include "../../include/blb_rs.h"
 #include "../../blb_amd/host/client.hpp"
 #include "../../blb_amd/host/reedsolomon.hpp"
 #include "../../blb_amd/host/tractserver.hpp"
@@ -641,6 +642,101 @@ static void TestRSEncodeConcurrentBatched(T* t) {
     if (launches >= requests) t->Errorf("no launch was shared (%llu launches)", (unsigned long long)launches);
 }
 
+// crc32.Update(crc, crc32.MakeTable(crc32.Castagnoli), p), bitwise: this test's own checker.
+static uint32_t crc32cUpdate(uint32_t crc, const uint8_t* p, size_t n) {
+    crc = ~crc;
+    for (size_t i = 0; i < n; ++i) {
+        crc ^= p[i];
+        for (int b = 0; b < 8; ++b) crc = (crc & 1u) ? (crc >> 1) ^ 0x82F63B78u : crc >> 1;
+    }
+    return ~crc;
+}
+
+extern "C" int hipDeviceSynchronize(void);  // the *_dev calls are asynchronous on the null stream
+
+// The recovery write path (curator reconstructChunk -> RSEncode with an indexMap, store.go:
+// 1102-1120): the missing pieces are rebuilt and CtlWrite'n to new hosts whose ChecksumFile
+// checksums them in 65532-byte blocks (pkg/disk/checksum_block.go:76-81).
+// blbrs_reconstruct_crc_dev_at does both in one pass; here on a window at file offset 4 MiB
+// (phase 256) continuing per-shard seeds, for fused shapes (RS(6,3) data-only and mixed,
+// RS(12,5) three erasures) and the (5,5) fallback (decode, then the CRC kernel).  Stripes live
+// in pinned host memory (device-accessible), checked against the bytes they held and this
+// file's bitwise CRC-32C.
+static void TestRecoveryWriteCRC(T* t) {
+    struct Case { int k, m; std::vector<int> lost; int data_only; };
+    const Case cases[] = {{6, 3, {1}, 1}, {6, 3, {0, 7}, 0}, {12, 5, {3, 9, 13}, 0}, {5, 5, {2, 6}, 0}, {6, 3, {2, 8}, 1}};
+    const size_t S = 200000, block = 65532, phase = 256, B = 2;
+    const size_t nblocks = (phase + S + block - 1) / block;
+    std::mt19937_64 rng(2024);
+    for (const Case& c : cases) {
+        const int n = c.k + c.m;
+        const size_t shard_stride = S + 64, stripe_stride = static_cast<size_t>(n) * shard_stride;
+        blbrs_encoder* enc = nullptr;
+        if (blbrs_new(c.k, c.m, &enc) != BLBRS_OK) Fatalf("New(%d,%d): %s", c.k, c.m, blbrs_last_error());
+        std::vector<int> rows;
+        for (int i : c.lost)
+            if (i < c.k) rows.push_back(i);
+        if (!c.data_only)
+            for (int i : c.lost)
+                if (i >= c.k) rows.push_back(i);
+        std::sort(rows.begin(), rows.begin() + std::count_if(rows.begin(), rows.end(), [&](int i) { return i < c.k; }));
+        void *mem = nullptr, *seed_mem = nullptr, *crc_mem = nullptr;
+        if (blbrs_host_alloc(B * stripe_stride, &mem) != BLBRS_OK ||
+            blbrs_host_alloc(rows.size() * B * 4, &seed_mem) != BLBRS_OK ||
+            blbrs_host_alloc(rows.size() * B * nblocks * 4, &crc_mem) != BLBRS_OK)
+            Fatalf("host_alloc: %s", blbrs_last_error());
+        uint8_t* st = static_cast<uint8_t*>(mem);
+        auto* seeds = static_cast<uint32_t*>(seed_mem);
+        auto* crc = static_cast<uint32_t*>(crc_mem);
+        std::vector<Bytes> truth;
+        for (size_t b = 0; b < B; ++b) {
+            std::vector<uint8_t*> ptrs(n);
+            std::vector<size_t> lens(n, S);
+            for (int i = 0; i < n; ++i) ptrs[i] = st + b * stripe_stride + i * shard_stride;
+            for (int i = 0; i < c.k; ++i) {
+                Bytes r = randBytes(rng, S);
+                std::memcpy(ptrs[i], r.data(), S);
+            }
+            if (blbrs_encode(enc, ptrs.data(), lens.data()) != BLBRS_OK) Fatalf("Encode: %s", blbrs_last_error());
+            for (int i = 0; i < n; ++i) truth.push_back(Bytes::copy_of(ptrs[i], S));
+        }
+        for (size_t j = 0; j < rows.size() * B; ++j) seeds[j] = static_cast<uint32_t>(rng());
+        std::vector<uint8_t> present(n, 1);
+        for (int i : c.lost) present[i] = 0;
+        for (size_t b = 0; b < B; ++b)
+            for (int i : c.lost) std::memset(st + b * stripe_stride + i * shard_stride, 0xA5, S);
+        int rc = blbrs_reconstruct_crc_dev_at(enc, st, shard_stride, stripe_stride, B, S, present.data(), c.data_only,
+                                              block, phase, seeds, crc, nullptr);
+        if (rc != BLBRS_OK) Fatalf("RS(%d,%d): reconstruct_crc: %s", c.k, c.m, blbrs_last_error());
+        if (hipDeviceSynchronize() != 0) Fatalf("hipDeviceSynchronize failed");
+        for (size_t b = 0; b < B; ++b)
+            for (int i : c.lost) {
+                const uint8_t* got = st + b * stripe_stride + i * shard_stride;
+                const bool rebuilt = std::find(rows.begin(), rows.end(), i) != rows.end();
+                if (rebuilt && std::memcmp(got, truth[b * n + i].data(), S) != 0)
+                    t->Errorf("RS(%d,%d) stripe %zu shard %d: wrong bytes", c.k, c.m, b, i);
+                if (!rebuilt && (got[0] != 0xA5 || got[S - 1] != 0xA5))
+                    t->Errorf("RS(%d,%d) stripe %zu: data-only call touched parity %d", c.k, c.m, b, i);
+            }
+        for (size_t j = 0; j < rows.size(); ++j)
+            for (size_t b = 0; b < B; ++b) {
+                const uint8_t* shard = truth[b * n + rows[j]].data();
+                for (size_t blk = 0; blk < nblocks; ++blk) {
+                    const size_t lo = blk * block > phase ? blk * block - phase : 0;
+                    const size_t hi = std::min(S, (blk + 1) * block - phase);
+                    const uint32_t want = crc32cUpdate(blk == 0 ? seeds[j * B + b] : 0u, shard + lo, hi - lo);
+                    const uint32_t got = crc[(j * B + b) * nblocks + blk];
+                    if (got != want)
+                        t->Errorf("RS(%d,%d) row %zu stripe %zu block %zu: crc %08x want %08x", c.k, c.m, j, b, blk, got, want);
+                }
+            }
+        blbrs_host_free(mem);
+        blbrs_host_free(seed_mem);
+        blbrs_host_free(crc_mem);
+        blbrs_free(enc);
+    }
+}
+
 int main(int argc, char** argv) {
     const bool cpu_only = argc > 1 && std::string(argv[1]) == "--cpu";
     struct Test { const char* name; void (*fn)(T*); bool gpu; };
@@ -664,6 +760,7 @@ int main(int argc, char** argv) {
         {"TestRSEncodeStopsAtFailingWrite", [](T* t) { TestRSEncodeStopsAtFailingWrite(t, false); }, true},
         {"TestRSEncodeStopsAtFailingWrite/pipelined", [](T* t) { TestRSEncodeStopsAtFailingWrite(t, true); }, true},
         {"TestRSEncodeConcurrentBatched", TestRSEncodeConcurrentBatched, true},
+        {"TestRecoveryWriteCRC", TestRecoveryWriteCRC, true},
     };
     int failed = 0, ran = 0;
     for (const Test& tc : tests) {

@@ -45,5 +45,6 @@ def test_cpp_mirror_cpu_asan():
 def test_cpp_mirror_gpu():
     out = _run(_build("_build/rs_test"))
     for name in ("TestRSEncode", "TestRSEncode/pipelined", "TestRSReconstruct", "TestRSReconstruct/pipelined",
-                 "TestReconstructDataIntoCallerBuffer", "TestClientRecovery", "TestPackThenRSEncode"):
+                 "TestReconstructDataIntoCallerBuffer", "TestClientRecovery", "TestPackThenRSEncode",
+                 "TestRecoveryWriteCRC"):
         assert f"--- PASS: {name}\n" in out, name

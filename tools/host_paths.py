@@ -9,7 +9,11 @@
     way concurrent RSEncode RPCs (internal/tractserver/store.go:1099) and degraded reads
     (client/blb/reconstruct.go:173) call it, with and without a Batcher attached (concurrent
     calls share launches).
-Prints one JSON object.  `--pool-only` runs just the pool-call sections."""
+  * the client's degraded-read shape (client/blb/reconstruct.go:172-173): ReconstructData
+    of one stripe whose k inputs are pool buffers and whose output is the user's pageable
+    Blob.ReadAt buffer (blob.go:59), 1 and 8 MiB pieces from 1..16 threads.
+Prints one JSON object.  `--pool-only` runs just the pool-call sections, `--client-only`
+just the client shape (BLBRS_LIB_PATH = an older build gives the "before" numbers)."""
 from __future__ import annotations
 
 import json
@@ -42,6 +46,11 @@ def timeit(fn, reps):
 def main():
     dev = torch.device("cuda:0")
     out = {}
+    if "--client-only" in sys.argv:
+        out["client_shape"] = client_shape(6, 3)
+        out["lib"] = os.environ.get("BLBRS_LIB_PATH") or "blb_amd/libblbrs.so"
+        print(json.dumps(out))
+        return
     if "--pool-only" in sys.argv:
         out["pool_calls"] = pool_calls(6, 3)
         out["pool_calls_batched"] = pool_calls(6, 3, window_us=50)
@@ -110,7 +119,57 @@ def main():
                                                    "cpu_threads": threads}
     out["pool_calls"] = pool_calls(k, m)
     out["pool_calls_batched"] = pool_calls(k, m, window_us=50)
+    out["client_shape"] = client_shape(k, m)
     print(json.dumps(out))
+
+
+def client_shape(k, m, seconds=1.5):
+    """reconstructOneTract's call: data[i] = pool-buffer replies (rpc.GetBuffer ->
+    blbrs_buffer_get, pinned), data[target] = thisB[0:0:length], a slice of the user's
+    pageable buffer; ReconstructData.  T threads, each its own stripe; GiB/s of data (k
+    pieces per call)."""
+    res = {}
+    target = 2
+    for S in (1 * MIB, 8 * MIB):
+        enc = rs.New(k, m, devices=[0])
+        for T in (1, 2, 4, 8, 16):
+            stripes = []
+            for t in range(T):
+                sh = [rs.GetBuffer(S) for _ in range(k + m)]
+                rng = np.random.default_rng(t)
+                for i in range(k):
+                    sh[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+                enc.Encode(sh)
+                truth = sh[target].copy()
+                thisB = np.empty(S + 4096, np.uint8)   # pageable, as Blob.ReadAt's p
+                stripes.append((sh, truth, thisB))
+            counts = [0] * T
+            ok = [True] * T
+            stop = time.perf_counter() + seconds
+
+            def loop(t):
+                sh, truth, thisB = stripes[t]
+                while time.perf_counter() < stop:
+                    work = list(sh)
+                    work[target] = None
+                    enc.ReconstructData(work, outs={target: thisB})
+                    counts[t] += 1
+                ok[t] = bool(np.array_equal(thisB[:S], truth))
+
+            t0 = time.perf_counter()
+            th = [threading.Thread(target=loop, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            el = time.perf_counter() - t0
+            res[f"{S // MIB}MiB_T{T}_GiBps_data"] = round(sum(counts) * k * S / GIB / el, 2)
+            res[f"{S // MIB}MiB_T{T}_calls_per_s"] = round(sum(counts) / el, 1)
+            res[f"{S // MIB}MiB_T{T}_ok"] = all(ok)
+            for sh, _, _ in stripes:
+                for b in sh:
+                    rs.PutBuffer(b)
+    return res
 
 
 def pool_calls(k, m, window_us=None):
