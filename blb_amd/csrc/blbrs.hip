@@ -388,22 +388,32 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         (void)hipStreamSynchronize(w->s[1]);
         return rc_;
     };
-    // Per-slot addressing: pinned (or device) shards are read and written in place by the
-    // kernels -- zero copy, over PCIe for pinned host memory, both link directions busy at once
-    // (RS(6,3): 50.8 GiB/s of data vs 37.3 through copy engines) -- and only
-    // pageable shards go through the worker's staging ring.  blb's degraded read has k pool
-    // buffers in and the user's pageable Blob.ReadAt buffer out (client/blb/reconstruct.go:
-    // 172-173, blob.go:59): one staged slot, not k + 1.
+    // Per-slot addressing: device shards are always used in place; pinned host shards are read
+    // and written in place by the kernels (zero copy over PCIe, both link directions busy at
+    // once) and only pageable shards go through the worker's staging ring.  blb's degraded read
+    // has k pool buffers in and the user's pageable Blob.ReadAt buffer out (client/blb/
+    // reconstruct.go:172-173, blob.go:59): one staged slot, not k + 1.  A read-dominated call
+    // under concurrency stages its pinned shards too, by DMA (rt::zero_copy_policy).
+    int nwritten = 0, ntouched = 0;
+    for (int i = 0; i < n; ++i) {
+        nwritten += is_out[i];
+        ntouched += touched[i];
+    }
+    const bool zero_copy = rt::zero_copy_policy(dev, nwritten, ntouched);
     std::vector<uint64_t> view(batch * n, 0);
     std::vector<char> pageable(batch * n, 0);
-    int max_staged = 0;  // pageable touched slots of the worst stripe
+    int max_staged = 0;  // staged touched slots of the worst stripe
     for (size_t b = 0; b < batch; ++b) {
         int ns = 0;
-        for (int i = 0; i < n; ++i)
-            if (touched[i] && !rt::device_view(shards[b * n + i], &view[b * n + i])) {
+        for (int i = 0; i < n; ++i) {
+            if (!touched[i]) continue;
+            int owner = -1;
+            const bool visible = rt::device_view(shards[b * n + i], &view[b * n + i], &owner);
+            if (!visible || (!zero_copy && owner < 0)) {
                 pageable[b * n + i] = 1;
                 ++ns;
             }
+        }
         max_staged = std::max(max_staged, ns);
     }
     if (max_staged == 0) {

@@ -71,14 +71,22 @@ constexpr int lc_index(int lc) { return lc == 32 ? 0 : 1; }
 //        (tables 8..15); table t, nibble k, value v at [t * kNibStride + 16 * k + v] is the
 //        matrix applied to v << 4k.  16 lookups per value instead of 32 columns x 2 VALU.
 //   wavemat[w] = S_{64*LC*(3-w)} (row end -> tile end), column-major.
-// tab8[k][i] = CRC of byte i followed by k zero bytes (slicing-by-8).
+// tab[k][i] = CRC of byte i followed by k zero bytes (slicing-by-kSlice uses tables 0..kSlice-1).
 constexpr uint32_t kNibStride = 136;  // 128 + 8 words: the 16 tables start on 8 different banks
 constexpr uint32_t kNibWords = 16 * kNibStride;
 struct TileConsts {
     uint32_t nib[2][kNibWords];
     uint32_t wavemat[2][4][32];
-    uint32_t tab8[8][256];
+    uint32_t tab[32][256];
 };
+
+// Slicing width of the chains: 8 (4 dependent steps per 32-byte lane chunk, 8 KiB of tables
+// per workgroup), 16 (2 steps, 16 KiB) or 32 (no dependent step, 32 KiB).
+#ifndef BLBRS_ECT_SLICE
+#define BLBRS_ECT_SLICE 8
+#endif
+constexpr int kSlice = BLBRS_ECT_SLICE;
+static_assert(kSlice == 8 || kSlice == 16 || kSlice == 32, "slicing width");
 
 // Coefficient loads one input pair behind the accumulators (0 = unconstrained): without it
 // all K*MR*5 table words are loaded up front and spill SGPRs (RS(12,5): 300 words, 70
@@ -89,9 +97,10 @@ struct TileConsts {
 constexpr int kTabSeq = BLBRS_ECT_TABSEQ;
 
 // 1 = the split wave's second pass zeroes the acc dwords before the boundary in place, so the
-// chain loop carries no per-dword masks (A/B builds).
+// chain loop carries no per-dword masks: RS(12,5) 14.15-14.41 vs 14.25-14.43 ms, RS(6,3)
+// 12.60-12.97 vs 12.68-12.95 (profiles/r03/ect_ab).  0 = the masked loop (A/B builds).
 #ifndef BLBRS_ECT_MASKACC
-#define BLBRS_ECT_MASKACC 0
+#define BLBRS_ECT_MASKACC 1
 #endif
 constexpr int kMaskAcc = BLBRS_ECT_MASKACC;
 // N > 0 = persistent grid of N workgroups per CU, each walking its XCD's tiles in a loop with
@@ -113,7 +122,7 @@ struct TArgs {
     uint32_t tps_full;        // whole tiles per stripe (the main grid); tps - 1 when S % T != 0
     const CrcConsts* c;
     const uint32_t* nib;      // [kNibWords] for this LC
-    const uint32_t* tab8;     // [8][256]
+    const uint32_t* tab8;     // [kSlice][256] (the first kSlice tables of TileConsts::tab)
     const uint32_t* wavemat;  // [4][32] for this LC
     uint32_t* raw;            // [(j * B + b) * tps + tile]: raw CRC of the tile's bytes
     uint32_t* hi;             // same index: raw CRC of the bytes past the tile's block boundary
@@ -134,10 +143,20 @@ struct TArgs {
     return r32[0] ^ r32[1];
 }
 
+// 1 = each nibble-table address is v_bfe + v_lshl_add (the nibble is made opaque so the
+// compiler does not rewrite it as shift + and + add, 3 VALU).
+#ifndef BLBRS_ECT_NIB2
+#define BLBRS_ECT_NIB2 0
+#endif
+
 __device__ __forceinline__ uint32_t apply_nib(const uint32_t* t, uint32_t c) {
     uint32_t v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = t[16 * k + __builtin_amdgcn_ubfe(c, 4 * k, 4)];
+    for (int k = 0; k < 8; ++k) {
+        uint32_t nb = __builtin_amdgcn_ubfe(c, 4 * k, 4);
+        if constexpr (BLBRS_ECT_NIB2) asm volatile("" : "+v"(nb));
+        v[k] = t[16 * k + nb];
+    }
     return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
 }
 
@@ -182,6 +201,26 @@ __device__ __forceinline__ uint32_t slice8(const uint32_t* tab, uint32_t x, uint
     return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
 }
 
+// XOR of N values, three at a time (v_bitop3).
+template <int N>
+__device__ __forceinline__ uint32_t xor_tree(const uint32_t* v) {
+    if constexpr (N == 1) return v[0];
+    else if constexpr (N == 2) return v[0] ^ v[1];
+    else return xor3(xor_tree<N / 3>(v), xor_tree<N / 3>(v + N / 3), xor_tree<N - 2 * (N / 3)>(v + 2 * (N / 3)));
+}
+
+// One slicing-by-SL step over SL / 4 dwords: d[0] already holds crc ^ first dword.  Byte k of
+// dword q uses table SL-1-4q-k; the lookups are independent of one another.
+template <int SL>
+__device__ __forceinline__ uint32_t slice_n(const uint32_t* tab, const uint32_t* d) {
+    uint32_t v[SL];
+#pragma unroll
+    for (int q = 0; q < SL / 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 * q + k] = tab[(SL - 1 - 4 * q - k) * 256 + __builtin_amdgcn_ubfe(d[q], 8 * k, 8)];
+    return xor_tree<SL>(v);
+}
+
 // The CRC part of one tile: this lane's LC contiguous parity bytes per row (acc, already in
 // lane_contiguous order) -> raw / hi of the tile, written by waves 0 and 1.  `red` is the
 // workgroup's reduction buffer (2 x 4 x MR words); one __syncthreads inside.
@@ -219,14 +258,30 @@ __device__ __forceinline__ void crc_tile(const TArgs& a, uint32_t (&acc)[MR][LC 
 #pragma unroll
                     for (int j = 0; j < MR; ++j) acc[j][d] = mine + 4u * d >= o ? acc[j][d] : 0u;
         }
+        if constexpr (kSlice == 8) {
 #pragma unroll
-        for (int d = 0; d < NV; d += 2) {
-            const bool keep0 = kMaskAcc || pass == 0 || mine + 4u * d >= o;
-            const bool keep1 = kMaskAcc || pass == 0 || mine + 4u * d + 4u >= o;
+            for (int d = 0; d < NV; d += 2) {
+                const bool keep0 = kMaskAcc || pass == 0 || mine + 4u * d >= o;
+                const bool keep1 = kMaskAcc || pass == 0 || mine + 4u * d + 4u >= o;
 #pragma unroll
-            for (int j = 0; j < MR; ++j) {
-                const uint32_t x = crc[j] ^ (keep0 ? acc[j][d] : 0u), y = keep1 ? acc[j][d + 1] : 0u;
-                crc[j] = (kFlags & 2) ? x ^ y : slice8(tab, x, y);
+                for (int j = 0; j < MR; ++j) {
+                    const uint32_t x = crc[j] ^ (keep0 ? acc[j][d] : 0u), y = keep1 ? acc[j][d + 1] : 0u;
+                    crc[j] = (kFlags & 2) ? x ^ y : slice8(tab, x, y);
+                }
+            }
+        } else {
+            static_assert(kMaskAcc, "wide slicing needs the in-place mask");
+            constexpr int W = kSlice / 4 < NV ? kSlice / 4 : NV;
+#pragma unroll
+            for (int d = 0; d < NV; d += W) {
+#pragma unroll
+                for (int j = 0; j < MR; ++j) {
+                    uint32_t w[W];
+#pragma unroll
+                    for (int q = 0; q < W; ++q) w[q] = acc[j][d + q];
+                    w[0] ^= crc[j];
+                    crc[j] = (kFlags & 2) ? w[0] ^ w[W - 1] : slice_n<4 * W>(tab, w);
+                }
             }
         }
         if constexpr (kFlags & 4) {
@@ -342,13 +397,16 @@ __device__ __forceinline__ void code_tile(const TArgs& a, uint8_t* stripe, uint6
 // second B-workgroup launch so that the masking never touches the main kernel).  Several
 // tiles per workgroup (constants staged once, the next tile's loads issued under this
 // tile's CRC) held 149-197 VGPRs and lost 5-7 % (r2g).
+// Wide-slicing builds hold the main instantiations to 3 waves per SIMD (RS(12,5) lands one
+// VGPR past 168 otherwise); the partial-tile launch (B workgroups) is left unconstrained.
 template <int K, int MR, int LC, bool PARTIAL>
-__global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
+__global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu((PARTIAL || kSlice == 8) ? 1 : 3)))
+void encode_crc_tile_kernel(TArgs a) {
     constexpr int NV = LC / 4;
     constexpr uint32_t kRow = 64u * LC;
     constexpr uint32_t kTile = 4u * kRow;
-    __shared__ uint32_t tab[8 * 256];
-    __shared__ uint32_t nib[kNibWords];
+    __shared__ __attribute__((aligned(16))) uint32_t tab[kSlice * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t nib[kNibWords];
     __shared__ uint32_t red[2][4][MR];
     __shared__ uint32_t wm[96];  // S_{64*LC*(3-w)}, w < 3
 
@@ -371,12 +429,16 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     const uint32_t lim = PARTIAL ? static_cast<uint32_t>(a.S - tile_off) : kTile;
 
     // Constants (L2 hits) into registers first, then the data loads: the LDS writes below
-    // wait for the constants only (in-order vmcnt).
-    constexpr int kFill = 8 * 256 / kTThreads;                          // table words per thread
-    constexpr int kNFill = (kNibWords + kTThreads - 1) / kTThreads;     // nibble-table words
+    // wait for the constants only (in-order vmcnt).  Wide slicing tables (16-32 KiB, 16-byte
+    // vectors) are loaded after the data, so their registers are not held while the inputs
+    // are in flight.
+    constexpr int kFill = kSlice == 8 ? 8 * 256 / kTThreads : 1;            // slicing-by-8 words
+    constexpr int kFillV = kSlice == 8 ? 1 : kSlice * 256 / 4 / kTThreads;  // wide: vectors
+    constexpr int kNFill = (kNibWords + kTThreads - 1) / kTThreads;         // nibble-table words
     uint32_t tv[kFill], nv[kNFill];
+    if constexpr (kSlice == 8)
 #pragma unroll
-    for (int r = 0; r < kFill; ++r) tv[r] = (kFlags & 1) ? tid * 3u + r : a.tab8[tid + r * kTThreads];
+        for (int r = 0; r < kFill; ++r) tv[r] = (kFlags & 1) ? tid * 3u + r : a.tab8[tid + r * kTThreads];
 #pragma unroll
     for (int r = 0; r < kNFill; ++r) {
         const uint32_t i = tid + r * kTThreads;
@@ -385,8 +447,18 @@ __global__ __launch_bounds__(kTThreads) void encode_crc_tile_kernel(TArgs a) {
     const uint32_t wmv = tid < 96u ? a.wavemat[tid] : 0u;
     uint32_t x[K][NV];
     load_tile<K, LC, PARTIAL>(a, stripe, tile_off, in_tile, lim, x);
+    if constexpr (kSlice == 8) {
 #pragma unroll
-    for (int r = 0; r < kFill; ++r) tab[tid + r * kTThreads] = tv[r];
+        for (int r = 0; r < kFill; ++r) tab[tid + r * kTThreads] = tv[r];
+    } else {
+        const u32x4* tsrc = reinterpret_cast<const u32x4*>(a.tab8);
+        u32x4 tw[kFillV];
+#pragma unroll
+        for (int r = 0; r < kFillV; ++r)
+            tw[r] = (kFlags & 1) ? u32x4{tid, 3u, 5u, static_cast<uint32_t>(r)} : tsrc[tid + r * kTThreads];
+#pragma unroll
+        for (int r = 0; r < kFillV; ++r) reinterpret_cast<u32x4*>(tab)[tid + r * kTThreads] = tw[r];
+    }
 #pragma unroll
     for (int r = 0; r < kNFill; ++r) {
         const uint32_t i = tid + r * kTThreads;
@@ -414,13 +486,13 @@ void encode_crc_tile_persist_kernel(TArgs a) {
     constexpr int NV = LC / 4;
     constexpr uint32_t kRow = 64u * LC;
     constexpr uint32_t kTile = 4u * kRow;
-    __shared__ uint32_t tab[8 * 256];
+    __shared__ uint32_t tab[kSlice * 256];
     __shared__ uint32_t nib[kNibWords];
     __shared__ uint32_t red[2][2][4][MR];
     __shared__ uint32_t wm[96];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (uint32_t i = tid; i < 8u * 256u; i += kTThreads) tab[i] = a.tab8[i];
+    for (uint32_t i = tid; i < kSlice * 256u; i += kTThreads) tab[i] = a.tab8[i];
     for (uint32_t i = tid; i < kNibWords; i += kTThreads) nib[i] = a.nib[i];
     if (tid < 96u) wm[tid] = a.wavemat[tid];
     __syncthreads();
@@ -600,11 +672,11 @@ hipError_t tile_consts_for(const TileConsts** out) {
         for (uint32_t i = 0; i < 256; ++i) {
             uint32_t v = i;
             for (int j = 0; j < 8; ++j) v = (v & 1u) ? (v >> 1) ^ kCrcPoly : v >> 1;
-            host.tab8[0][i] = v;
+            host.tab[0][i] = v;
         }
-        for (int k = 1; k < 8; ++k)
+        for (int k = 1; k < 32; ++k)
             for (uint32_t i = 0; i < 256; ++i)
-                host.tab8[k][i] = (host.tab8[k - 1][i] >> 8) ^ host.tab8[0][host.tab8[k - 1][i] & 255u];
+                host.tab[k][i] = (host.tab[k - 1][i] >> 8) ^ host.tab[0][host.tab[k - 1][i] & 255u];
         for (int v = 0; v < 2; ++v) {
             const uint64_t lc = v == 0 ? 32 : 16;
             uint32_t col[32];
@@ -691,7 +763,7 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     a.c = c;
     a.nib = &tc->nib[lc_index(lc)][0];
     a.wavemat = &tc->wavemat[lc_index(lc)][0][0];
-    a.tab8 = &tc->tab8[0][0];
+    a.tab8 = &tc->tab[0][0];
     const uint64_t tiles = static_cast<uint64_t>(in.B) * a.tps;
     const uint64_t groups = static_cast<uint64_t>(in.B) * a.tps_full;  // one tile per workgroup
     a.xcd_remap = groups % 8 == 0 ? 1u : 0u;

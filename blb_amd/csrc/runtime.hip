@@ -208,6 +208,11 @@ int lane_stats(int dev, int occ, blbrs_lane_stats* out) {
     return BLBRS_OK;
 }
 
+bool zero_copy_policy(int dev, int written, int touched) {
+    if (const char* env = std::getenv("BLBRS_HOST_ZC"); env && *env) return env[0] != '0';
+    return 4 * written >= touched || load_of(dev) <= kZeroCopyMaxCalls;
+}
+
 bool device_view(const void* p, uint64_t* view, int* owner) {
     if (owner) *owner = -1;
     hipPointerAttribute_t attr;

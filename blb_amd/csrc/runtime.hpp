@@ -88,6 +88,16 @@ struct LoadTicket {
     ~LoadTicket();
 };
 
+// Whether a host call codes its pinned host shards in place (zero copy over PCIe) or stages
+// them by DMA like pageable ones (tools/host_paths.py --zc-sweep): zero copy
+// wins at every concurrency when the call writes at least a quarter of the slots it touches
+// (Encode: the kernel's posted writes run beside its reads), and for read-dominated calls
+// (ReconstructData: k in, 1 out) while at most kZeroCopyMaxCalls host calls are in flight on
+// the device (this one included); beyond that the copy engines move the inputs faster.
+// $BLBRS_HOST_ZC = 1 / 0 (read per call) forces either way for A/B runs.
+constexpr int64_t kZeroCopyMaxCalls = 3;
+bool zero_copy_policy(int dev, int written, int touched);
+
 // Address under which the GPU reaches `p`: device memory as is, pinned host memory
 // (hipHostMalloc / hipHostRegister) through its device mapping.  False for pageable memory.
 // *owner = the device holding device memory, -1 for host memory.

@@ -2,7 +2,10 @@
 // pinned buffer pool (blbrs_buffer_get): pooled, NOT zeroed, capacity classes of 1, 4 and
 // 8 MiB + 64 KiB.  Shards on such buffers are coded in place by the GPU (zero-copy).  The
 // buffer goes back to the pool when the last Bytes holding it is dropped -- the
-// PutBuffer(b, true) of store.go:1048-1052.  Without a usable GPU it falls back to make().
+// PutBuffer(b, true) of store.go:1048-1052, and a Bytes that is simply dropped releases it
+// too (the GC semantics blb relies on: reconstruct.go:126-152 drops straggling replies).
+// Without a usable GPU, or past the engine's pinned live limit (BLBRS_ERR_LIMIT), it falls
+// back to make(): pageable memory, which the engine stages.
 #pragma once
 #include <cstring>
 

@@ -30,7 +30,7 @@ from typing import Optional, Protocol, Sequence
 
 import numpy as np
 
-from . import pack, reedsolomon
+from . import pack, reedsolomon, rpc
 from .blbcore import (ENCODE_INCREMENT_PROD, RS_CHUNK_VERSION, TRACT_LENGTH, Error, RSChunkID,
                       TractID, TSAddr)
 
@@ -209,7 +209,7 @@ class Store:
         try:
             if encode:
                 for data_i in imap[N:]:
-                    data[data_i] = np.empty(length, dtype=np.uint8)  # rpc.GetBuffer: not zeroed
+                    data[data_i] = rpc.GetBuffer(length)  # store.go:1099: not zeroed
                 enc.Encode(data)
             else:
                 reconstruct_and_verify(enc, data)
@@ -231,6 +231,19 @@ class Store:
                 return e
         return Error.NoError
 
+    @staticmethod
+    def _release(data):
+        """store.go:1048-1052: `defer rpc.PutBuffer(b, true)` for everything in data."""
+        for b in data or ():
+            if b is not None:
+                rpc.PutBuffer(b, True)
+
+    def _scatter_release(self, baseid, offset, dests, imap, N, data):
+        try:
+            return self._scatter(baseid, offset, dests, imap, N, data)
+        finally:
+            self._release(data)
+
     def _rs_encode_one(self, baseid, offset, length, srcs, dests, index_map, enc) -> Error:
         N, M = len(srcs), len(dests)
         imap, encode = self._index_map(N, M, index_map)
@@ -239,10 +252,13 @@ class Store:
         data, err = self._gather(baseid, offset, length, srcs, imap, N, M)
         if err != Error.NoError:
             return err
-        err = self._code(enc, data, encode, imap, N, length)
-        if err != Error.NoError:
-            return err
-        return self._scatter(baseid, offset, dests, imap, N, data)
+        try:
+            err = self._code(enc, data, encode, imap, N, length)
+            if err != Error.NoError:
+                return err
+            return self._scatter(baseid, offset, dests, imap, N, data)
+        finally:
+            self._release(data)
 
     def _rs_encode_pipelined(self, baseid, windows, srcs, dests, index_map, enc) -> Error:
         """Software pipeline over windows: gather(i+1) || scatter(i), code(i) || scatter(i-1)."""
@@ -260,6 +276,7 @@ class Store:
                     return err
                 err = self._code(enc, data, encode, imap, N, ln)
                 if err != Error.NoError:
+                    self._release(data)
                     return err
                 if pending_write is not None:
                     err = pending_write.result()
@@ -270,7 +287,7 @@ class Store:
                 if i + 1 < len(windows):
                     o2, l2 = windows[i + 1]
                     nxt = stage.submit(self._gather, baseid, o2, l2, srcs, imap, N, M)
-                pending_write = stage.submit(self._scatter, baseid, off, dests, imap, N, data)
+                pending_write = stage.submit(self._scatter_release, baseid, off, dests, imap, N, data)
             return pending_write.result() if pending_write is not None else Error.NoError
         finally:
             stage.shutdown(wait=True)

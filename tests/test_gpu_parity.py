@@ -376,6 +376,44 @@ def test_baseline_rs104_b512_two_erasures(oracle_lib, dev):
     torch.cuda.empty_cache()
 
 
+def test_cold_class_rs83_b512_full_size(oracle_lib, dev):
+    """blb's COLD transition class RS(8,3) (targetClass, internal/curator/
+    storage_class_loop.go:41-44) at the bench's size: 512 stripes of 8 MiB.  Encode
+    (oracle-checked stripes), Verify, 1- and 2-erasure rebuilds (data and mixed), and the
+    fused encode + ChecksumFile CRCs of rsEncodeOne's parity window at file offset 4 MiB
+    (phase 256, seeded), checked against the oracle's crc32.Update per file-aligned block."""
+    k, m, B, S = 8, 3, 512, TRACT
+    enc = rs.New(k, m)
+    st = torch.empty((B, k + m, S), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(8303)
+    st[:, :k].random_(0, 256, generator=g)
+    enc.EncodeBatch(st)
+    _sample_check(oracle_lib, enc, st, k, m, [0, 255, 511])
+    assert bool(enc.VerifyBatch(st).all())
+    for pat, data_only in (([1], True), ([1, 5], False), ([3, 9], False)):
+        saved = st[:, pat].clone()
+        st[:, pat] = 0xA5
+        enc.ReconstructBatch(st, [i not in pat for i in range(k + m)], data_only=data_only)
+        assert torch.equal(st[:, pat], saved), pat
+    seeds = torch.randint(-2**31, 2**31 - 1, (m, B), dtype=torch.int32, device=dev)
+    st[:, k:] = 0x5A
+    crc = enc.EncodeBatchCRC(st, 65532, phase=256, seeds=seeds)
+    assert bool(enc.VerifyBatch(st).all())
+    crc = crc.cpu().numpy().view(np.uint32)
+    sd = seeds.cpu().numpy().view(np.uint32)
+    first = 65532 - 256
+    for b in (0, 511):
+        par = st[b, k:].cpu().numpy()
+        for j in range(m):
+            want0 = oracle_lib.crc32c(par[j][:first], int(sd[j, b]))
+            rest = np.asarray(oracle_lib.crc32c_blocks(par[j][first:], 65532), dtype=np.uint32)
+            assert crc[j, b, 0] == want0, (b, j)
+            assert np.array_equal(crc[j, b, 1:], rest), (b, j)
+    del st, seeds
+    torch.cuda.empty_cache()
+
+
 def _pinned(a):
     return torch.from_numpy(a).pin_memory().numpy()
 

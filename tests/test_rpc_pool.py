@@ -329,8 +329,8 @@ def test_degraded_reads_drop_buffers_pinned_bounded(oracle_lib, delayed_gc):
     rpc.gc()
     gc.collect()
     assert rs.pool_stats()["registered_bytes"] == st0["registered_bytes"] == 0, rs.pool_stats()
-    assert rpc.stats["unregistered"] - r0["unregistered"] == rpc.stats["registered"] - r0["registered"] + \
-        rpc.stats["reregistered"] - r0["reregistered"]
+    # every registration (first ones and re-registrations of reused pageable buffers) undone
+    assert rpc.stats["unregistered"] - r0["unregistered"] == rpc.stats["registered"] - r0["registered"]
 
 
 # ---------------------------------------------------------------- GPU: host CRC staging

@@ -46,6 +46,19 @@ def timeit(fn, reps):
 def main():
     dev = torch.device("cuda:0")
     out = {}
+    if "--zc-sweep" in sys.argv:
+        # Zero-copy vs DMA staging of pinned shards (BLBRS_HOST_ZC, read per call), and the
+        # library's default policy, on the pool-buffer calls and the client shape.
+        for mode in ("1", "0", "auto"):
+            if mode == "auto":
+                os.environ.pop("BLBRS_HOST_ZC", None)
+            else:
+                os.environ["BLBRS_HOST_ZC"] = mode
+            out[f"zc_{mode}"] = {"pool_calls": pool_calls(6, 3, seconds=1.0), "client_shape": client_shape(6, 3, 1.0)}
+            print(json.dumps({mode: out[f"zc_{mode}"]}), file=sys.stderr, flush=True)
+        os.environ.pop("BLBRS_HOST_ZC", None)
+        print(json.dumps(out))
+        return
     if "--client-only" in sys.argv:
         out["client_shape"] = client_shape(6, 3)
         out["lib"] = os.environ.get("BLBRS_LIB_PATH") or "blb_amd/libblbrs.so"
@@ -172,7 +185,7 @@ def client_shape(k, m, seconds=1.5):
     return res
 
 
-def pool_calls(k, m, window_us=None):
+def pool_calls(k, m, window_us=None, seconds=2.0):
     """Per-call host Encode / ReconstructData of one stripe of 4 MiB pool buffers per call,
     T threads each looping over its own stripe for ~2 s; with `window_us`, through a Batcher
     (max_batch 32) attached to the encoder."""
@@ -195,7 +208,7 @@ def pool_calls(k, m, window_us=None):
             stripes.append(sh)
         for op in ("encode", "reconstruct_data1"):
             counts = [0] * T
-            stop = time.perf_counter() + 2.0
+            stop = time.perf_counter() + seconds
 
             def loop(t):
                 sh = stripes[t]

@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1); } } while (0)
 
@@ -96,7 +97,25 @@ void run(uint32_t B) {
     fflush(stdout);
 }
 
-int main() {
+int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "rs83") {
+        // RS(8,3) pack + encode, bench.py's cold_class_extras: 512 stripes, the tracts fill
+        // 5.7 of the 8 data pieces (24.5 GB read), 11 shards written (pieces + parity).
+        const uint32_t B = 512;
+        CK(hipMalloc(&g_src, size_t(B) * 8 * S + 64));  // R <= 8 source shards per stripe
+        CK(hipMalloc(&g_dst, size_t(B) * 11 * S));
+        CK(hipMemset(g_src, 0x3C, size_t(B) * 8 * S + 64));
+        for (int rep = 0; rep < 2; ++rep) {
+            printf("# rep %d\n", rep);
+            run<8, 3, 2, false>(B);    // the RS(8,3) encode's mix
+            run<6, 11, 1, false>(B);   // pack + encode, aligned sources
+            run<6, 11, 1, true>(B);    // misaligned sources (two loads + v_alignbyte)
+            run<6, 11, 2, false>(B);
+            run<0, 11, 1, false>(B);   // pure write
+            run<0, 11, 4, false>(B);
+        }
+        return 0;
+    }
     // 1024 stripes' worth of the pack+encode mix: 4 reads x 8 MiB + 9 writes x 8 MiB per stripe.
     const uint32_t B = 1024;
     CK(hipMalloc(&g_src, size_t(B) * 6 * S + 64));
