@@ -153,6 +153,21 @@ __global__ __launch_bounds__(kThreads) void crc_segment_kernel(SegArgs a) {
 // its real end; the bytes before its start are virtual zeros: rows wholly inside that prefix
 // are skipped (a zero prefix leaves the raw CRC at 0), the row holding the start is loaded
 // dword by dword, and the rest run through a branch-free loop that loads one row ahead.
+// Rows of the register ring: loads run kRing - 1 rows ahead of the row being checksummed.
+#ifndef BLBRS_CRC_RING
+#define BLBRS_CRC_RING 3
+#endif
+constexpr int kRing = BLBRS_CRC_RING;
+// 2 = each wave runs two chains at once, over rows 0-7 and 8-15 of its segment (joined with
+// S_{32 KiB}), halving the dependent LDS steps per row consumed (A/B builds).
+#ifndef BLBRS_CRC_ILP
+#define BLBRS_CRC_ILP 1
+#endif
+constexpr int kIlp = BLBRS_CRC_ILP;
+#ifndef BLBRS_CRC_XCD
+#define BLBRS_CRC_XCD 0
+#endif
+constexpr bool kXcdMap = BLBRS_CRC_XCD != 0;
 constexpr int kStreamThreads = 1024;
 constexpr uint32_t kChunk = 64, kRowBytes = kChunk * 64, kRows = 16;  // 4 KiB rows
 constexpr uint32_t kWaveSeg = kRowBytes * kRows;                      // 64 KiB per wave
@@ -193,6 +208,49 @@ __device__ __forceinline__ Chunk load_row(const uint8_t* p) {
     return ch;
 }
 
+// BLBRS_CRC_COAL: 1 = each wave instruction loads a contiguous 1 KiB sub-row (lane_piece
+// order) and v_permlane swaps give every lane its 64 contiguous bytes at use; 2 = the same
+// with nontemporal loads (A/B builds).
+#ifndef BLBRS_CRC_COAL
+#define BLBRS_CRC_COAL 0
+#endif
+constexpr int kCoal = BLBRS_CRC_COAL;
+
+__device__ __forceinline__ Chunk load_row_at(const uint8_t* lane_chunk, const uint8_t* row, uint32_t lane) {
+    if constexpr (kCoal == 0) {
+        return load_row(lane_chunk);
+    } else {
+        Chunk ch;
+        const uint8_t* p = row + lane_piece<64>(lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            ch.q[q] = kCoal == 2 ? __builtin_nontemporal_load(reinterpret_cast<const V4x*>(p + 1024 * q))
+                                 : *reinterpret_cast<const V4x*>(p + 1024 * q);
+        return ch;
+    }
+}
+
+// A coalesced row into lane-contiguous order (no-op for the per-lane layout).
+__device__ __forceinline__ Chunk to_lane(const Chunk& in) {
+    if constexpr (kCoal == 0) {
+        return in;
+    } else {
+        uint32_t v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            v[4 * q] = in.q[q].x;
+            v[4 * q + 1] = in.q[q].y;
+            v[4 * q + 2] = in.q[q].z;
+            v[4 * q + 3] = in.q[q].w;
+        }
+        lane_contiguous<64>(v);
+        Chunk out;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out.q[i] = V4x{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+        return out;
+    }
+}
+
 // 4 waves per SIMD is fixed by the 1024-thread workgroup + 128 KiB LDS; saying so lets the
 // scheduler spend VGPRs on load-ahead instead of sinking loads next to their uses.
 __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void crc_stream_kernel(
@@ -207,7 +265,16 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const cu32 gap = as_const(a.c->gap[0]);
     const cu32 wlvl = as_const(&a.c->wlvl[0][0][0]);
-    for (uint64_t g = blockIdx.x * (kStreamThreads / 64) + wave; g < a.total_segs; g += waves) {
+    // Segments in dispatch order, or (BLBRS_CRC_XCD) each XCD's workgroups walking one
+    // contiguous eighth of them.
+    uint64_t g_lo = blockIdx.x * (kStreamThreads / 64) + wave, g_hi = a.total_segs, g_step = waves;
+    if (kXcdMap && gridDim.x % 8u == 0) {
+        const uint32_t x = blockIdx.x % 8u;
+        g_lo = a.total_segs * x / 8u + (blockIdx.x / 8u) * (kStreamThreads / 64) + wave;
+        g_hi = a.total_segs * (x + 1u) / 8u;
+        g_step = waves / 8u;
+    }
+    for (uint64_t g = g_lo; g < g_hi; g += g_step) {
         const uint32_t s = static_cast<uint32_t>(g % a.segs_per_block);
         const uint32_t blk = static_cast<uint32_t>((g / a.segs_per_block) % a.nblocks);
         const uint64_t b = g / (static_cast<uint64_t>(a.segs_per_block) * a.nblocks);
@@ -230,9 +297,9 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
         if (pad < kRowBytes) {
             // Common case (every segment of 65532-byte blocks and of whole dword frames): only
             // row 0 can hold virtual zeros.  Straight-line code, loads two rows ahead.
-            Chunk ring[3];
+            Chunk ring[kRing];
             if (pad == 0) {
-                ring[0] = load_row(lane_base);
+                if constexpr (!kCoal) ring[0] = load_row(lane_base);
             } else {
                 // Row 0 through a buffer resource based at the segment start and bounded to
                 // row 0's real bytes: dwords before the start have negative (wrapped) offsets,
@@ -249,18 +316,58 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
                     ring[0].q[i] = V4x{w[0], w[1], w[2], w[3]};
                 }
             }
-            ring[1] = load_row(lane_base + kRowBytes);
-            ring[2] = load_row(lane_base + 2 * kRowBytes);
+            if constexpr (kIlp == 2) {
+                // Chain A over rows 0..7, chain B over rows 8..15, a ring per chain.
+                constexpr uint32_t kHalf = kRows / 2;
+                Chunk rb[kRing];
+#pragma unroll
+                for (int r = 1; r < kRing; ++r) ring[r] = load_row(lane_base + r * kRowBytes);
+#pragma unroll
+                for (int r = 0; r < kRing; ++r) rb[r] = load_row(lane_base + (kHalf + r) * kRowBytes);
+                __builtin_amdgcn_sched_barrier(0);
+                uint32_t cb = 0;
+#pragma unroll
+                for (uint32_t r = 0; r < kHalf; ++r) {
+                    const Chunk ca_cur = ring[r % kRing], cb_cur = rb[r % kRing];
+                    if (r + kRing < kHalf) {
+                        ring[r % kRing] = load_row(lane_base + (r + kRing) * kRowBytes);
+                        rb[r % kRing] = load_row(lane_base + (kHalf + r + kRing) * kRowBytes);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (r) {
+                        c = apply(gap, c);
+                        cb = apply(gap, cb);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        c = slice4(t, c ^ ca_cur.q[i].x);
+                        cb = slice4(t, cb ^ cb_cur.q[i].x);
+                        c = slice4(t, c ^ ca_cur.q[i].y);
+                        cb = slice4(t, cb ^ cb_cur.q[i].y);
+                        c = slice4(t, c ^ ca_cur.q[i].z);
+                        cb = slice4(t, cb ^ cb_cur.q[i].z);
+                        c = slice4(t, c ^ ca_cur.q[i].w);
+                        cb = slice4(t, cb ^ cb_cur.q[i].w);
+                    }
+                }
+                c = apply(as_const(&a.c->pow2[15][0]), c) ^ cb;  // S_{8 rows = 32 KiB}
+            } else {
+            const uint8_t* row0 = lane_base - lane * kChunk;
+            if (kCoal && pad == 0) ring[0] = load_row_at(lane_base, row0, lane);
+#pragma unroll
+            for (int r = 1; r < kRing; ++r) ring[r] = load_row_at(lane_base + r * kRowBytes, row0 + r * kRowBytes, lane);
             // sched_barrier pins each row's loads where they are issued; left alone the
             // scheduler sinks them next to their first use and every row waits on HBM.
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (uint32_t r = 0; r < kRows; ++r) {
-                const Chunk cur = ring[r % 3];
-                if (r + 3 < kRows) ring[r % 3] = load_row(lane_base + (r + 3) * kRowBytes);
+                const Chunk cur = (r == 0 && pad != 0) ? ring[0] : to_lane(ring[r % kRing]);
+                if (r + kRing < kRows)
+                    ring[r % kRing] = load_row_at(lane_base + (r + kRing) * kRowBytes, row0 + (r + kRing) * kRowBytes, lane);
                 __builtin_amdgcn_sched_barrier(0);
                 if (r) c = apply(gap, c);
                 c = crc_chunk(t, c, cur);
+            }
             }
         } else {
             // Short tail segment: rows before the start are all zeros (raw CRC stays 0).
