@@ -198,9 +198,10 @@ __device__ __forceinline__ uint32_t crc_chunk(const LaneTabs& t, uint32_t c, con
     return c;
 }
 
-// Plain (L1-allocating) loads: each 128-byte line is split over the four dwordx4
-// instructions of two lanes, and the L1 merges them; nontemporal loads bypass that merge
-// and measured 1.6x slower (3.3 vs 5.3 TB/s).
+// Per-lane layout (BLBRS_CRC_COAL=0): plain (L1-allocating) loads, because each 128-byte
+// line is split over the four dwordx4 instructions of two lanes and the L1 merges them;
+// nontemporal loads bypass that merge and measured 1.6x slower (3.3 vs 5.3 TB/s).  The
+// coalesced layout below has no split lines, so it can stream nontemporal.
 __device__ __forceinline__ Chunk load_row(const uint8_t* p) {
     Chunk ch;
 #pragma unroll
@@ -208,11 +209,14 @@ __device__ __forceinline__ Chunk load_row(const uint8_t* p) {
     return ch;
 }
 
-// BLBRS_CRC_COAL: 1 = each wave instruction loads a contiguous 1 KiB sub-row (lane_piece
-// order) and v_permlane swaps give every lane its 64 contiguous bytes at use; 2 = the same
-// with nontemporal loads (A/B builds).
+// Row loads.  0 = lane t loads its own 64 contiguous bytes (four dwordx4 64 bytes apart: each
+// instruction touches 64 partial lines that the L1 merges); 1 = each wave instruction loads a
+// contiguous 1 KiB sub-row (lane_piece order) and v_permlane swaps give every lane its 64
+// contiguous bytes at use; 2 (default) = 1 with nontemporal loads.  3072 x 8 MiB rows:
+// 65532-byte blocks 4.40-4.49 ms (2) vs 4.69 (1) vs 4.78-4.89 (0), whole rows 4.28-4.37 vs
+// 4.68-4.71 vs 4.52-4.57 (profiles/r03/crc_ab).
 #ifndef BLBRS_CRC_COAL
-#define BLBRS_CRC_COAL 0
+#define BLBRS_CRC_COAL 2
 #endif
 constexpr int kCoal = BLBRS_CRC_COAL;
 
@@ -320,18 +324,22 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
                 // Chain A over rows 0..7, chain B over rows 8..15, a ring per chain.
                 constexpr uint32_t kHalf = kRows / 2;
                 Chunk rb[kRing];
+                const uint8_t* row0 = lane_base - lane * kChunk;
+                auto ld = [&](uint32_t r) { return load_row_at(lane_base + r * kRowBytes, row0 + r * kRowBytes, lane); };
+                if (kCoal && pad == 0) ring[0] = ld(0);
 #pragma unroll
-                for (int r = 1; r < kRing; ++r) ring[r] = load_row(lane_base + r * kRowBytes);
+                for (int r = 1; r < kRing; ++r) ring[r] = ld(r);
 #pragma unroll
-                for (int r = 0; r < kRing; ++r) rb[r] = load_row(lane_base + (kHalf + r) * kRowBytes);
+                for (int r = 0; r < kRing; ++r) rb[r] = ld(kHalf + r);
                 __builtin_amdgcn_sched_barrier(0);
                 uint32_t cb = 0;
 #pragma unroll
                 for (uint32_t r = 0; r < kHalf; ++r) {
-                    const Chunk ca_cur = ring[r % kRing], cb_cur = rb[r % kRing];
+                    const Chunk ca_cur = (r == 0 && pad != 0) ? ring[0] : to_lane(ring[r % kRing]);
+                    const Chunk cb_cur = to_lane(rb[r % kRing]);
                     if (r + kRing < kHalf) {
-                        ring[r % kRing] = load_row(lane_base + (r + kRing) * kRowBytes);
-                        rb[r % kRing] = load_row(lane_base + (kHalf + r + kRing) * kRowBytes);
+                        ring[r % kRing] = ld(r + kRing);
+                        rb[r % kRing] = ld(kHalf + r + kRing);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                     if (r) {

@@ -144,36 +144,45 @@ var (
 	buf8MBPool = sync.Pool{New: func() interface{} { return newPinned(buf8MBSize) }}
 	buf4MBPool = sync.Pool{New: func() interface{} { return newPinned(buf4MBSize) }}
 	buf1MBPool = sync.Pool{New: func() interface{} { return newPinned(buf1MBSize) }}
-	// Base addresses of the class buffers currently registered with the engine.
-	pinned sync.Map // uintptr -> struct{}
+	// The class buffers this pool allocated, by base address (a uintptr key keeps nothing
+	// alive).  Only these are ever registered: a foreign slice put back with a class
+	// capacity (pool.go allows any buffer) stays as it is.
+	owned sync.Map // uintptr -> *poolBuf
 )
 
-// register pins b's backing array with the engine and arranges for it to be unpinned when the
-// GC collects it.  b must be a whole class buffer (b[0] is the start of its allocation).
-func register(b []byte) {
-	p := &b[0]
-	addr := uintptr(unsafe.Pointer(p))
-	if C.blbrs_buffer_register(unsafe.Pointer(p), C.size_t(len(b))) != C.BLBRS_OK {
-		return // live limit reached (or no GPU): the buffer stays pageable
-	}
-	pinned.Store(addr, struct{}{})
-	runtime.SetFinalizer(p, func(p *byte) {
-		pinned.Delete(uintptr(unsafe.Pointer(p)))
-		C.blbrs_buffer_unregister(unsafe.Pointer(p))
-	})
-}
+type poolBuf struct{ pinned atomic.Bool }
 
+// newPinned allocates a class buffer, ties its bookkeeping to the GC and pins it if the live
+// limit allows.  The finalizer runs when the backing array is unreachable, before its memory
+// is freed: it unpins the buffer (the engine keeps the registered address only until then;
+// coding calls touch the memory only while their caller holds the slice).
 func newPinned(size int) interface{} {
 	b := make([]byte, size)
-	register(b)
+	p := &b[0]
+	pb := &poolBuf{}
+	owned.Store(uintptr(unsafe.Pointer(p)), pb)
+	runtime.SetFinalizer(p, func(p *byte) {
+		if v, ok := owned.LoadAndDelete(uintptr(unsafe.Pointer(p))); ok && v.(*poolBuf).pinned.Load() {
+			C.blbrs_buffer_unregister(unsafe.Pointer(p))
+		}
+	})
+	pin(b, pb)
 	return &b
+}
+
+// pin registers a whole class buffer with the engine (BLBRS_ERR_LIMIT or no GPU: it stays
+// pageable, which the engine stages).
+func pin(b []byte, pb *poolBuf) {
+	if C.blbrs_buffer_register(unsafe.Pointer(&b[0]), C.size_t(len(b))) == C.BLBRS_OK {
+		pb.pinned.Store(true)
+	}
 }
 
 func getClass(pool *sync.Pool, n int) []byte {
 	b := *pool.Get().(*[]byte)
 	b = b[:cap(b)] // a put slice may be shorter; its cap is the class size
-	if _, ok := pinned.Load(uintptr(unsafe.Pointer(&b[0]))); !ok {
-		register(b) // refused earlier: try again now that it is reused
+	if v, ok := owned.Load(uintptr(unsafe.Pointer(&b[0]))); ok && !v.(*poolBuf).pinned.Load() {
+		pin(b, v.(*poolBuf)) // refused earlier: try again now that it is reused
 	}
 	return b[:n]
 }
