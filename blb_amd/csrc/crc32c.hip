@@ -202,7 +202,7 @@ __device__ __forceinline__ uint32_t crc_chunk(const LaneTabs& t, uint32_t c, con
 // line is split over the four dwordx4 instructions of two lanes and the L1 merges them;
 // nontemporal loads bypass that merge and measured 1.6x slower (3.3 vs 5.3 TB/s).  The
 // coalesced layout below has no split lines, so it can stream nontemporal.
-__device__ __forceinline__ Chunk load_row(const uint8_t* p) {
+[[maybe_unused]] __device__ __forceinline__ Chunk load_row(const uint8_t* p) {
     Chunk ch;
 #pragma unroll
     for (int i = 0; i < 4; ++i) ch.q[i] = *reinterpret_cast<const V4x*>(p + 16 * i);

@@ -7,6 +7,7 @@ BASELINE size, plus calibration kernels of known traffic in the same process:
   reconstruct     ReconstructBatch, data shard 1 missing        (rs_code_kernel, 1 row)
   verify          VerifyBatch                                   (rs_code_kernel, verify)
   encode_crc      EncodeBatchCRC(65532)                         (encode_crc_tile_kernel + combine)
+  crc32c          ChecksumBatch of parity shard k, 65532 blocks (crc_stream_kernel)
 
 Markers: the dispatch order is fixed; tools/pmc_prod_summary.py matches kernels by name and
 order.  Prints the libblbrs.so sha256 it loaded."""
@@ -45,6 +46,9 @@ torch.cuda.synchronize()
 ok = enc.VerifyBatch(st)
 torch.cuda.synchronize()
 crc = enc.EncodeBatchCRC(st, 65532)
+torch.cuda.synchronize()
+from blb_amd import checksum  # noqa: E402
+crc1 = checksum.ChecksumBatch(st[:, k], 65532)  # crc32c: parity shard k of every stripe
 torch.cuda.synchronize()
 lib = _lib.LIB_PATH
 print(json.dumps({"lib": lib, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),

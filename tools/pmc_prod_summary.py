@@ -63,7 +63,7 @@ def main():
     k, m, B, S = meta["k"], meta["m"], meta["batch"], meta["shard"]
 
     # calibration: the copy kernel that follows the fill (both 8 GiB)
-    big = [x for x in fetch if "rs_code" not in x[1] and "encode_crc" not in x[1]]
+    big = [x for x in fetch if "rs_code" not in x[1] and "encode_crc" not in x[1] and "crc_stream" not in x[1]]
     copy_f = max(big, key=lambda x: x[2].get("FETCH_SIZE", 0.0))
     f_scale = 8 * GIB / (copy_f[2]["FETCH_SIZE"] * 1024.0)
     bigw = [x for x in write if x[0] == copy_f[0]]
@@ -81,7 +81,8 @@ def main():
             ("reconstruct_data1", "rs_code_kernel", 1, B * (k + 1) * S),
             ("verify", "rs_code_kernel", 2, B * (k + m) * S),
             ("encode_crc_65532", "encode_crc_tile_kernel", 0, B * (k + m) * S),
-            ("encode_crc_combine", "tile_combine_kernel", 0, None)]
+            ("encode_crc_combine", "tile_combine_kernel", 0, None),
+            ("crc32c_65532", "crc_stream_kernel", 0, B * S)]
     for label, needle, nth, algo in spec:
         f = pick(fetch, needle, nth)
         w = pick(write, needle, nth)
