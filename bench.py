@@ -502,6 +502,15 @@ def main():
         extra["verify"] = {"GiBps_data": round(B * k * S / GIB / (ver_ms * 1e-3), 2),
                            "ms_per_launch": round(ver_ms, 3), "all_ok": flags_ok,
                            "hbm_GBps_algorithmic": round(B * (k + m) * S / (ver_ms * 1e-3) / 1e9, 1)}
+        # reconstructAndVerify (store.go:1132-1142, the recovery RPC): Reconstruct of data
+        # shard 1 then Verify as two passes, against the one-pass store+verify kernel.
+        rv_two = _ev_ms(lambda: (enc.ReconstructBatch(stripes, present), enc.VerifyBatch(stripes)),
+                        max(3, a.steps // 4), stream, dev)
+        rv_ok = bool(enc.ReconstructAndVerifyBatch(stripes, present).all())
+        rv_one = _ev_ms(lambda: enc.ReconstructAndVerifyBatch(stripes, present), max(3, a.steps // 4), stream, dev)
+        extra["reconstruct_and_verify_1_data_erasure"] = {
+            "one_pass_ms": round(rv_one, 3), "two_pass_ms": round(rv_two, 3), "speedup": round(rv_two / rv_one, 3),
+            "hbm_GBps_algorithmic_one_pass": round(algo_bytes / (rv_one * 1e-3) / 1e9, 1), "verify_ok": rv_ok}
         # CRC-32C of every parity shard in 65532-byte ChecksumFile blocks (§8f row 2).
         from blb_amd import checksum
         # Parity rows are strided (k+m)*S apart: checksum them as m strided batches of B rows.

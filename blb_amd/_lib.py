@@ -31,6 +31,7 @@ SIGNATURES = {
     "blbrs_reconstruct_dev_ptrs": (_I, [_P, _P, _SZ, _SZ, _P, _I, _P]),
     "blbrs_verify_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P, _P]),
     "blbrs_verify_dev_ptrs": (_I, [_P, _P, _SZ, _SZ, _P, _P]),
+    "blbrs_reconstruct_verify_dev": (_I, [_P, _P, _SZ, _SZ, _SZ, _SZ, _P, _P, _P]),
     "blbrs_encode_host_batch": (_I, [_P, _P, _SZ, _SZ, _I]),
     "blbrs_crc32c_dev": (_I, [_P, _SZ, _SZ, _SZ, _SZ, _P, _P]),
     "blbrs_crc32c": (_I, [_P, _SZ, _SZ, _P]),

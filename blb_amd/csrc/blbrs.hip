@@ -57,6 +57,7 @@ namespace {
 // One kernel pass: <= kMaxRows output rows over k_in inputs.
 struct Pass {
     int k_in = 0, rows = 0;
+    int nstore = -1;  // store+verify plans: rows [0, nstore) of this pass are stored
     std::vector<int32_t> in_idx, out_idx;
     std::vector<uint32_t> tables;
 };
@@ -67,6 +68,8 @@ struct HostPlan {
     std::vector<int32_t> in_idx;   // inputs (shard indices)
     std::vector<int32_t> out_idx;  // outputs (shard indices), one per row
     Mat rows;                      // out_idx.size() x k_in
+    int nstore = -1;               // store+verify plan: the first nstore rows are written, the
+                                   // rest compared (-1: a plain store / verify plan)
     std::vector<Pass> passes;
 };
 
@@ -76,6 +79,7 @@ void split_passes(HostPlan& p) {
         Pass ps;
         ps.k_in = p.k_in;
         ps.rows = std::min(kMaxRows, nrows - r0);
+        if (p.nstore >= 0) ps.nstore = std::max(0, std::min(ps.rows, p.nstore - r0));
         ps.in_idx = p.in_idx;
         ps.out_idx.assign(p.out_idx.begin() + r0, p.out_idx.begin() + r0 + ps.rows);
         Mat sub(p.rows.begin() + static_cast<size_t>(r0) * p.k_in,
@@ -92,6 +96,7 @@ struct DevPass {
     const int32_t* out_idx = nullptr;
     const uint32_t* tables = nullptr;
     int k_in = 0, rows = 0;
+    int nstore = -1;
 };
 struct DevPlan {
     std::vector<DevPass> passes;
@@ -112,6 +117,7 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
         DevPass d;
         d.k_in = ps.k_in;
         d.rows = ps.rows;
+        d.nstore = ps.nstore;
         const size_t n_in = ps.in_idx.size() * 4, n_out = round_up(ps.out_idx.size() * 4, 16);
         const size_t off_out = round_up(n_in, 16), off_tab = off_out + n_out;
         const size_t bytes = off_tab + ps.tables.size() * 4;
@@ -131,11 +137,12 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
     return BLBRS_OK;
 }
 
-std::string plan_key(bool encode, const std::vector<uint8_t>& present, bool data_only) {
+// "E" = encode; "R" + ('d' data only | 'a' all | 'v' all + verify) + present bits.
+std::string plan_key(bool encode, const std::vector<uint8_t>& present, bool data_only, bool verify = false) {
     if (encode) return "E";
     std::string key(present.size() + 2, '0');
     key[0] = 'R';
-    key[1] = data_only ? 'd' : 'a';
+    key[1] = verify ? 'v' : data_only ? 'd' : 'a';
     for (size_t i = 0; i < present.size(); ++i) key[i + 2] = present[i] ? '1' : '0';
     return key;
 }
@@ -215,6 +222,52 @@ struct EncoderCore {
         return slot;
     }
 
+    // reconstructAndVerify in one pass (store.go:1132-1142): inputs = the first k present
+    // shards, as for Reconstruct; rows = every missing shard (stored), then every present
+    // shard the decode does not read (compared).  Verify after Reconstruct recomputes the
+    // parity from the rebuilt data: the inputs and the rebuilt shards agree with it by
+    // construction (M[valid] * inv(M[valid]) = I), so what it checks is exactly the present
+    // shards outside the inputs -- all parity, since data shards come first.  k + m - k = m
+    // rows: every shard is read or written once (k + m shard passes instead of 2k + m + e).
+    std::shared_ptr<HostPlan> decode_verify_plan(const std::vector<uint8_t>& present, int* rc) {
+        const std::string key = plan_key(false, present, false, true);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = host_plans.find(key);
+            if (it != host_plans.end() && it->second) return it->second;
+        }
+        auto dp = decode_plan(present, false, rc);  // inputs, inverse, missing rows
+        if (!dp) return nullptr;
+        auto p = std::make_shared<HostPlan>();
+        p->k_in = dp->k_in;
+        p->in_idx = dp->in_idx;
+        p->out_idx = dp->out_idx;
+        p->rows = dp->rows;
+        p->nstore = static_cast<int>(dp->out_idx.size());
+        std::vector<uint8_t> is_in(k + m, 0);
+        for (int32_t i : p->in_idx) is_in[i] = 1;
+        // P[e] * inv(M[valid]) for the extra present shards: reuse the decode's inverse.
+        Mat sub(static_cast<size_t>(k) * k), dec;
+        for (int r = 0; r < k; ++r)
+            std::memcpy(&sub[static_cast<size_t>(r) * k], &matrix[static_cast<size_t>(p->in_idx[r]) * k], k);
+        if (!invert(sub, k, dec)) {
+            *rc = fail(BLBRS_ERR_SINGULAR, "matrix is singular");
+            return nullptr;
+        }
+        for (int i = 0; i < k + m; ++i)
+            if (present[i] && !is_in[i]) {
+                Mat row(matrix.begin() + static_cast<size_t>(i) * k, matrix.begin() + static_cast<size_t>(i + 1) * k);
+                Mat r = matmul(row, 1, k, dec, k);
+                p->out_idx.push_back(i);
+                p->rows.insert(p->rows.end(), r.begin(), r.end());
+            }
+        split_passes(*p);
+        std::lock_guard<std::mutex> g(mu);
+        auto& slot = host_plans[key];
+        if (!slot) slot = p;
+        return slot;
+    }
+
     // Device tables for `hp` on `device` (uploaded on first use; the caller has made
     // `device` current).
     int dev_plan(const std::string& key, const HostPlan& hp, int device, const DevPlan** out) {
@@ -244,6 +297,9 @@ struct blbrs_encoder {
     std::shared_ptr<HostPlan> encode_plan() { return core->encode_plan(); }
     std::shared_ptr<HostPlan> decode_plan(const std::vector<uint8_t>& present, bool data_only, int* rc) {
         return core->decode_plan(present, data_only, rc);
+    }
+    std::shared_ptr<HostPlan> decode_verify_plan(const std::vector<uint8_t>& present, int* rc) {
+        return core->decode_verify_plan(present, rc);
     }
     int dev_plan(const std::string& key, const HostPlan& hp, int device, const DevPlan** out) {
         return core->dev_plan(key, hp, device, out);
@@ -309,7 +365,12 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         a.rows = ps.rows;
         a.aligned = st.aligned ? 1 : 0;
         a.mismatch = mismatch;
-        hipError_t e = launch_code(a, mode, stream);
+        Mode m = mode;
+        if (mode == Mode::kStoreVerify) {  // per pass: all stored, all compared, or mixed
+            a.nstore = ps.nstore;
+            m = ps.nstore == ps.rows ? Mode::kStore : ps.nstore == 0 ? Mode::kVerify : Mode::kStoreVerify;
+        }
+        hipError_t e = launch_code(a, m, stream);
         if (e != hipSuccess) return hip_fail(e, "launch rs_code_kernel");
     }
     return BLBRS_OK;
@@ -372,9 +433,12 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             touched[i] = 1;
             if (!produced[i]) need_in[i] = 1;
         }
-        for (int32_t i : hp.out_idx) {
+        for (size_t r = 0; r < hp.out_idx.size(); ++r) {
+            const int32_t i = hp.out_idx[r];
             touched[i] = 1;
-            if (steps[t].mode == Mode::kStore) {
+            const bool store = steps[t].mode == Mode::kStore ||
+                               (steps[t].mode == Mode::kStoreVerify && static_cast<int>(r) < hp.nstore);
+            if (store) {
                 produced[i] = 1;
                 is_out[i] = 1;
             } else {
@@ -576,8 +640,9 @@ struct BatchReq {
     EncoderCore* core = nullptr;
     std::shared_ptr<HostPlan> hp;   // store step (encode / decode plan); null = verify only
     std::shared_ptr<HostPlan> vp;   // verify step after it (the encode plan); null = none
+    bool mixed = false;             // hp is a store+verify plan (reconstructAndVerify, one pass)
     std::string key;                // group key: plan key, "+V" when verifying
-    int ok = 0;                     // verify result (vp set)
+    int ok = 0;                     // verify result (vp set or mixed)
     std::vector<uint64_t> views;  // device-visible address per shard slot (0 = unused)
     size_t S = 0;
     int dev = -1;                 // device that must run it (device-memory shards), -1 = any
@@ -716,8 +781,18 @@ struct blbrs_batcher {
                 Stripes st;
                 st.nshards = static_cast<uint32_t>(n);
                 rc = upload(lane, table, &st.ptrs, &st.aligned);
-                if (rc == BLBRS_OK && plan)
+                if (rc == BLBRS_OK && plan && r0.mixed) {
+                    rc = flags(lane, reqs.size());
+                    if (rc == BLBRS_OK)
+                        rc = run_plan(*plan, st, reqs.size(), S, Mode::kStoreVerify, lane->flags_dev, lane->stream);
+                    if (rc == BLBRS_OK) {
+                        const hipError_t e = hipMemcpyAsync(lane->flags_host, lane->flags_dev, reqs.size() * 4,
+                                                            hipMemcpyDeviceToHost, lane->stream);
+                        if (e != hipSuccess) rc = hip_fail(e, "batched verify flags");
+                    }
+                } else if (rc == BLBRS_OK && plan) {
                     rc = run_plan(*plan, st, reqs.size(), S, Mode::kStore, nullptr, lane->stream);
+                }
                 if (rc == BLBRS_OK && vplan) {
                     rc = flags(lane, reqs.size());
                     if (rc == BLBRS_OK)
@@ -737,7 +812,7 @@ struct blbrs_batcher {
                 BatchReq* r = reqs[j];
                 r->rc = rc;
                 if (rc != BLBRS_OK) r->msg = rt::last_error();
-                else if (r->vp) r->ok = lane->flags_host[j] == 0;
+                else if (r->vp || r->mixed) r->ok = lane->flags_host[j] == 0;
             }
         }
         requests.fetch_add(batch.size());
@@ -789,12 +864,13 @@ namespace {
 // is the encode or decode plan (at least one output), `key` its cache key; argument checks
 // have been done.
 int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key, std::shared_ptr<HostPlan> hp,
-                 std::shared_ptr<HostPlan> vp, uint8_t* const* shards, size_t S, int* ok) {
+                 std::shared_ptr<HostPlan> vp, uint8_t* const* shards, size_t S, int* ok, bool mixed = false) {
     const int n = enc->k + enc->m;
     BatchReq req;
     req.core = enc->core.get();
     req.hp = hp;
     req.vp = vp;
+    req.mixed = mixed;
     req.key = vp ? key + "+V" : key;
     req.S = S;
     req.views.assign(n, 0);
@@ -803,7 +879,10 @@ int batched_call(blbrs_batcher* b, blbrs_encoder* enc, const std::string& key, s
     std::vector<char> touched(n, 0), written(n, 0);
     if (hp) {
         for (int32_t i : hp->in_idx) touched[i] = 1;
-        for (int32_t i : hp->out_idx) touched[i] = written[i] = 1;
+        for (size_t r = 0; r < hp->out_idx.size(); ++r) {
+            touched[hp->out_idx[r]] = 1;
+            if (!mixed || static_cast<int>(r) < hp->nstore) written[hp->out_idx[r]] = 1;
+        }
     }
     if (vp) {
         for (int32_t i : vp->in_idx) touched[i] = 1;
@@ -1038,16 +1117,26 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
     for (int32_t i : hp->out_idx)
         if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "missing shard has no output buffer");
+    // reconstructAndVerify: one pass that writes the missing shards and compares the present
+    // shards the decode does not read (EncoderCore::decode_verify_plan).
+    std::shared_ptr<HostPlan> vp;
+    if (verify_ok && !hp->out_idx.empty()) {
+        vp = enc->decode_verify_plan(present, &rc);
+        if (!vp) return rc;
+        for (int32_t i : vp->out_idx)
+            if (!shards[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
+    }
     if (b && !hp->out_idx.empty()) {
-        if ((rc = batched_call(b, enc, plan_key(false, present, data_only), hp, verify_ok ? ep : nullptr, shards, S,
-                               verify_ok)))
-            return rc;
+        rc = vp ? batched_call(b, enc, plan_key(false, present, false, true), vp, nullptr, shards, S, verify_ok, true)
+                : batched_call(b, enc, plan_key(false, present, data_only), hp, nullptr, shards, S, nullptr);
+        if (rc) return rc;
         for (int32_t i : hp->out_idx) lens[i] = S;
         return BLBRS_OK;
     }
     std::vector<Step> steps;
-    if (!hp->out_idx.empty()) steps.push_back(Step{plan_key(false, present, data_only), hp.get(), Mode::kStore});
-    if (verify_ok) steps.push_back(Step{"E", ep.get(), Mode::kVerify});
+    if (vp) steps.push_back(Step{plan_key(false, present, false, true), vp.get(), Mode::kStoreVerify});
+    else if (!hp->out_idx.empty()) steps.push_back(Step{plan_key(false, present, data_only), hp.get(), Mode::kStore});
+    else if (verify_ok) steps.push_back(Step{"E", ep.get(), Mode::kVerify});
     if (steps.empty()) return BLBRS_OK;  // data_only with only parity missing
     rc = host_call(enc, steps, shards, S, verify_ok);
     if (rc) return rc;
@@ -1199,6 +1288,30 @@ int blbrs_verify_dev(blbrs_encoder* enc, const uint8_t* stripes, size_t shard_st
         return rc;
     auto hp = enc->encode_plan();
     return dev_run(enc, dc.dev, "E", *hp, st, batch, shard_len, Mode::kVerify, mismatch_dev, stream);
+}
+
+int blbrs_reconstruct_verify_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, size_t stripe_stride,
+                                 size_t batch, size_t shard_len, const uint8_t* present, int32_t* mismatch_dev,
+                                 void* stream) {
+    if (!enc || !mismatch_dev || !present) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    auto pv = present_vec(enc, present);
+    int np = 0;
+    for (uint8_t x : pv) np += x;
+    if (np == enc->k + enc->m)  // nothing to rebuild: reconstructAndVerify is a Verify
+        return blbrs_verify_dev(enc, stripes, shard_stride, stripe_stride, batch, shard_len, mismatch_dev, stream);
+    if (np < enc->k) return fail(BLBRS_ERR_TOO_FEW_SHARDS, "too few shards given");
+    if (batch == 0) return BLBRS_OK;
+    DevCall dc;
+    int rc = dc.enter(mismatch_dev);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(mismatch_dev, 0, batch * sizeof(int32_t), static_cast<hipStream_t>(stream)));
+    if (shard_len == 0) return BLBRS_OK;
+    auto vp = enc->decode_verify_plan(pv, &rc);
+    if (!vp) return rc;
+    Stripes st;
+    if ((rc = dev_stripes_strided(stripes, shard_stride, stripe_stride, batch, shard_len, &st))) return rc;
+    return dev_run(enc, dc.dev, plan_key(false, pv, false, true), *vp, st, batch, shard_len, Mode::kStoreVerify,
+                   mismatch_dev, stream);
 }
 
 int blbrs_verify_dev_ptrs(blbrs_encoder* enc, const uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,

@@ -114,7 +114,7 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
         for (int r = 0; r < MR; ++r) {
             if (r >= nr) break;
             uint8_t* q = shard_ptr<ADDR>(a, b, as_const(a.out_idx)[r]) + off;
-            if constexpr (MODE == 0) {
+            if (MODE == 0 || (MODE == 2 && r < a.nstore)) {
                 if (vec) st16<0>(q, pack(acc[r]));
                 else store_bytes(q, pack(acc[r]), nb);
             } else if (neq(vec ? ld16<0>(q) : load_bytes(q, nb), pack(acc[r]))) {
@@ -127,7 +127,8 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
 // K > 0: compile-time input count (all K*U chunk loads issued before any math).
 // K == 0: runtime k (loads issued per input, two inputs unrolled).
 // MR: compile-time bound on output rows; a.rows <= MR honoured at runtime.
-// MODE 0 = store outputs, 1 = compare against existing outputs (Verify).
+// MODE 0 = store outputs, 1 = compare against existing outputs (Verify), 2 = store rows
+// [0, a.nstore) and compare the rest (reconstructAndVerify in one pass).
 // ADDR 0 = strided stripes, 1 = pointer table.  U = 16-byte chunks per lane per tile.
 template <int K, int MR, int MODE, int ADDR, int U, int NT>
 __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
@@ -161,11 +162,12 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
 
         // Verify: the shards to check are loaded up front with the inputs, so the whole
         // tile's reads are in flight before any math.
-        V4 chk[MODE == 1 ? MR : 1][U];
-        if constexpr (MODE == 1) {
+        V4 chk[MODE != 0 ? MR : 1][U];
+        if constexpr (MODE != 0) {
+            const int first_chk = MODE == 2 ? a.nstore : 0;
 #pragma unroll
             for (int r = 0; r < MR; ++r) {
-                if (r < nr) {
+                if (r < nr && r >= first_chk) {
                     const uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
 #pragma unroll
                     for (int u = 0; u < U; ++u) chk[r][u] = ld16<NT>(q + u * kStep);
@@ -221,20 +223,20 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
             }
         }
 
+        bool bad = false;
 #pragma unroll
         for (int r = 0; r < MR; ++r) {
             if (r >= nr) break;
             uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
-            if constexpr (MODE == 0) {
+            if (MODE == 0 || (MODE == 2 && r < a.nstore)) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) st16<NT>(q + u * kStep, pack(acc[r] + 4 * u));
             } else {
-                bool bad = false;
 #pragma unroll
                 for (int u = 0; u < U; ++u) bad |= neq(chk[r][u], pack(acc[r] + 4 * u));
-                flag_mismatch(a.mismatch + b, bad);
             }
         }
+        if constexpr (MODE != 0) flag_mismatch(a.mismatch + b, bad);
     }
 }
 
@@ -264,7 +266,7 @@ constexpr int kNT = 3;
 #define BLBRS_U_VERIFY_WIDE 1  // verify mode, K + MR > 13
 #endif
 constexpr int pick_u(int K, int MR, int MODE) {
-    return MODE == 0 ? ((K > 0 && K + MR <= 9) ? 4 : BLBRS_U_WIDE) : (K + MR > 13 ? BLBRS_U_VERIFY_WIDE : 2);
+    return MODE == 0 ? ((K > 0 && K + MR <= 9) ? 4 : BLBRS_U_WIDE) : (K + MR > 13 ? BLBRS_U_VERIFY_WIDE : 2);  // MODE 1, 2
 }
 
 template <int K, int MR, int MODE, int ADDR>
@@ -306,13 +308,16 @@ Choice pick_k(int k, int rows) {
 
 Choice pick(int k, int rows, Mode mode, bool strided) {
     if (mode == Mode::kStore) return strided ? pick_k<0, 0>(k, rows) : pick_k<0, 1>(k, rows);
-    return strided ? pick_k<1, 0>(k, rows) : pick_k<1, 1>(k, rows);
+    if (mode == Mode::kVerify) return strided ? pick_k<1, 0>(k, rows) : pick_k<1, 1>(k, rows);
+    return strided ? pick_k<2, 0>(k, rows) : pick_k<2, 1>(k, rows);
 }
 
 }  // namespace
 
 hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream) {
     if (args.rows < 1 || args.rows > kMaxRows || args.k < 1) return hipErrorInvalidValue;
+    if (mode != Mode::kStore && !args.mismatch) return hipErrorInvalidValue;
+    if (mode == Mode::kStoreVerify && (args.nstore < 0 || args.nstore > args.rows)) return hipErrorInvalidValue;
     if (args.B == 0 || args.S == 0) return hipSuccess;
     const Choice ch = pick(args.k, args.rows, mode, args.base != nullptr);
     if (!ch.fn) return hipErrorInvalidValue;

@@ -26,6 +26,7 @@ struct CodeArgs {
     int32_t aligned;          // every shard address 16-byte aligned (vector path allowed)
     int32_t* mismatch;        // verify: [B] flags (device)
     int32_t xcd_remap;        // set by launch_code(): block b starts at tile (b%8)*(grid/8) + b/8
+    int32_t nstore;           // kStoreVerify: rows [0, nstore) are stored, the rest compared
 };
 
 constexpr int kThreads = 256;
@@ -33,7 +34,10 @@ constexpr int kBytesPerThread = 16;                       // one dwordx4 per sha
 constexpr int kTileBytes = kThreads * kBytesPerThread;    // byte columns per block-iteration
 constexpr int kMaxRows = 8;                               // outputs per pass
 
-enum class Mode : int { kStore = 0, kVerify = 1 };
+// kStoreVerify: one pass of reconstructAndVerify (store.go:1132-1142) -- the first nstore
+// rows (the missing shards) are written, the others (present shards the decode did not read)
+// are compared, so every shard is read or written once.
+enum class Mode : int { kStore = 0, kVerify = 1, kStoreVerify = 2 };
 
 // Launches one pass over args.B stripes on `stream` (grid, tiles and XCD mapping chosen
 // here); returns hipSuccess or the launch error.

@@ -381,6 +381,21 @@ class Encoder:
                                                       int(data_only), blk, phase, sp, out.data_ptr(), st))
         return out
 
+    def ReconstructAndVerifyBatch(self, stripes, present: Sequence[bool], stream: Optional[int] = None):
+        """reconstructAndVerify (store.go:1132-1142) on a device batch in one pass: the shards
+        marked absent are rebuilt in place; returns a [B] torch.bool CUDA tensor, True where
+        the completed stripe verifies."""
+        import torch
+        B, S, ss, bs = self._stripes(stripes)
+        if len(present) != self.Shards:
+            raise ErrTooFewShards("too few shards given")
+        flags = torch.empty(B, dtype=torch.int32, device=stripes.device)
+        pres = (ctypes.c_uint8 * self.Shards)(*[1 if p else 0 for p in present])
+        st = _torch_stream(stripes) if stream is None else stream
+        _check(self._lib.blbrs_reconstruct_verify_dev(self._h, stripes.data_ptr(), ss, bs, B, S, pres,
+                                                      flags.data_ptr(), st))
+        return flags == 0
+
     def VerifyBatch(self, stripes, stream: Optional[int] = None):
         """Returns a [B] torch.bool CUDA tensor: True where the stripe's parity is consistent."""
         import torch

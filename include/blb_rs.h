@@ -146,8 +146,9 @@ int blbrs_reconstruct(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens);
 /* Encoder.ReconstructData: rebuild missing data shards only; parity slots untouched. */
 int blbrs_reconstruct_data(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens);
 
-/* reconstructAndVerify (internal/tractserver/store.go:1132-1142) in one device round trip:
- * Reconstruct, then Verify the completed stripe while it is still on the GPU.  Same
+/* reconstructAndVerify (internal/tractserver/store.go:1132-1142) in one device round trip
+ * and one kernel pass: the missing shards are written and the present shards the decode does
+ * not read are checked against it, which is what Verify after Reconstruct checks.  Same
  * arguments and errors as blbrs_reconstruct; *ok = 0 is store.go's errVerifyFailed. */
 int blbrs_reconstruct_verify(blbrs_encoder* enc, uint8_t* const* shards, size_t* lens, int* ok);
 
@@ -182,6 +183,17 @@ int blbrs_verify_dev(blbrs_encoder* enc, const uint8_t* stripes, size_t shard_st
                      int32_t* mismatch_dev, void* stream);
 int blbrs_verify_dev_ptrs(blbrs_encoder* enc, const uint8_t* const* shard_ptrs, size_t batch,
                           size_t shard_len, int32_t* mismatch_dev, void* stream);
+
+/* Batched reconstructAndVerify (internal/tractserver/store.go:1132-1142: Reconstruct, then
+ * Verify) in ONE pass over HBM, one erasure pattern for the batch: every missing shard (data
+ * and parity) is written, and mismatch_dev[b] (device, zeroed first) is set to 1 when stripe
+ * b fails the Verify that would follow.  The pass reads the k shards the decode uses and the
+ * other present shards, and writes the missing ones: k + m shards per stripe instead of the
+ * 2k + m + e of Reconstruct then Verify.  Nothing missing: a plain Verify.  The host-memory
+ * blbrs_reconstruct_verify and the batcher use the same pass. */
+int blbrs_reconstruct_verify_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride,
+                                 size_t stripe_stride, size_t batch, size_t shard_len,
+                                 const uint8_t* present, int32_t* mismatch_dev, void* stream);
 
 /* Multi-device batches: parts[p] is one device's share (the device that owns
  * parts[p].stripes), launched asynchronously on parts[p].stream -- the caller synchronizes

@@ -458,6 +458,48 @@ def test_streaming_host_batch_pageable_fallback(oracle_lib):
             assert np.array_equal(st[k + j], want[j])
 
 
+@pytest.mark.parametrize("k,m", [(3, 2), (6, 3), (8, 3), (10, 4), (12, 5), (5, 9)])
+def test_reconstruct_and_verify_one_pass_vs_oracle(oracle_lib, dev, k, m):
+    """reconstructAndVerify in one pass (missing shards written, the present shards the decode
+    does not read compared): the rebuilt bytes and the verdict equal the oracle's Reconstruct
+    then Verify for every erasure count, with a corrupted shard inside the decode's inputs
+    (the oracle's Verify then fails unless no shard is left over), a corrupted leftover
+    shard, and none; host path and device batch.  (5, 9): 14 rows, two kernel passes."""
+    n = k + m
+    rng = np.random.default_rng(k * 100 + m)
+    S = 70001
+    enc = rs.New(k, m)
+    full = rand_shards(rng, k, S) + [np.empty(S, np.uint8) for _ in range(m)]
+    oracle_lib.encode(k, m, full)
+    cases = 0
+    for e in range(1, m + 1):
+        lost = sorted(rng.choice(n, e, replace=False).tolist())
+        present = [i not in lost for i in range(n)]
+        inputs = [i for i in range(n) if present[i]][:k]
+        leftovers = [i for i in range(n) if present[i] and i not in inputs]
+        for corrupt in (None, inputs[-1], leftovers[0] if leftovers else None):
+            base = [x.copy() for x in full]
+            if corrupt is not None:
+                base[corrupt][S // 3] ^= 0x21
+            want = oracle_lib.reconstruct(k, m, [None if i in lost else base[i].copy() for i in range(n)], False)
+            want_ok = oracle_lib.verify(k, m, want)
+            cur = [None if i in lost else base[i].copy() for i in range(n)]
+            ok = enc.ReconstructAndVerify(cur)
+            assert ok == want_ok, (k, m, lost, corrupt)
+            for i in lost:
+                assert np.array_equal(cur[i], want[i]), (k, m, lost, corrupt, i)
+            st = torch.from_numpy(np.stack(base + base)).reshape(2, n, S).to(dev)
+            for i in lost:
+                st[:, i] = 0xA5
+            oks = enc.ReconstructAndVerifyBatch(st, present).cpu().numpy()
+            assert list(oks) == [want_ok, want_ok], (k, m, lost, corrupt)
+            got = st.cpu().numpy()
+            for i in lost:
+                assert np.array_equal(got[0, i], want[i]) and np.array_equal(got[1, i], want[i])
+            cases += 1
+    assert cases >= 2 * m
+
+
 def test_reconstruct_and_verify_fused(oracle_lib):
     """reconstructAndVerify (store.go:1132-1142) in one round trip: true for a consistent
     stripe (incl. when nothing is missing), false when a surviving shard disagrees."""
