@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -737,6 +738,170 @@ static void TestRecoveryWriteCRC(T* t) {
     }
 }
 
+// GF(2^8)/0x11D products for this file's own parity check (the library's matrix, this
+// file's arithmetic).
+struct GfTable {
+    uint8_t mul[256][256];
+    GfTable() {
+        for (int a = 0; a < 256; ++a)
+            for (int b = 0; b < 256; ++b) {
+                uint8_t p = 0, x = static_cast<uint8_t>(a);
+                for (int y = b; y; y >>= 1) {
+                    if (y & 1) p ^= x;
+                    x = static_cast<uint8_t>((x << 1) ^ ((x & 0x80) ? 0x1D : 0));
+                }
+                mul[a][b] = p;
+            }
+    }
+};
+
+// Host calls from many threads over the round-3 host runtime at once: two lanes on GPU 0
+// (device list [0, 0], routed by bytes in flight), per-slot addressing (pageable, pool and
+// registered slots mixed in one call), registrations refused by a small live limit (those
+// buffers stay pageable and are staged), the batcher's mixed path, and the one-pass
+// reconstructAndVerify with and without a corrupted shard.  Every output is checked against
+// parity computed here from the library's matrix.  The ThreadSanitizer build runs it
+// (profiles/r03/tsan).
+static void TestConcurrentHostSlots(T* t) {
+    const int k = 6, m = 3, n = k + m, threads = 8, iters = 10;
+    static const GfTable gf;
+    blbrs_pool_stats ps0{};
+    blbrs_get_pool_stats(&ps0);
+    // Room for a few registered shards beyond what is pinned now: the rest are refused.
+    if (blbrs_pool_set_live_limit(ps0.live_bytes + ps0.registered_bytes + (12u << 20)) != BLBRS_OK)
+        Fatalf("set_live_limit: %s", blbrs_last_error());
+    const int devs[2] = {0, 0};
+    blbrs_encoder *lanes = nullptr, *batched = nullptr;
+    blbrs_batcher* bat = nullptr;
+    if (blbrs_new_on(k, m, devs, 2, &lanes) != BLBRS_OK || blbrs_new_on(k, m, devs, 2, &batched) != BLBRS_OK ||
+        blbrs_batcher_new_on(16, 200, devs, 2, &bat) != BLBRS_OK || blbrs_encoder_set_batcher(batched, bat) != BLBRS_OK)
+        Fatalf("setup: %s", blbrs_last_error());
+    uint8_t mat[n * k];
+    blbrs_matrix(lanes, mat, sizeof(mat));
+
+    std::mutex emu;
+    std::vector<std::string> errors;
+    auto report = [&](const std::string& s) {
+        std::lock_guard<std::mutex> g(emu);
+        if (errors.size() < 20) errors.push_back(s);
+    };
+    std::atomic<int> refused{0}, mixed_calls{0};
+    std::vector<std::thread> th;
+    for (int w = 0; w < threads; ++w)
+        th.emplace_back([&, w] {
+            std::mt19937_64 rng(4242 + w);
+            for (int it = 0; it < iters; ++it) {
+                const size_t sizes[] = {4096, 65536 + 16 * (rng() % 512), 1 + rng() % (1u << 20), 1u << 20};
+                const size_t S = sizes[rng() % 4];
+                const size_t alloc = (S + 4095) / 4096 * 4096;
+                enum Kind { Pageable, Pool, Registered };
+                Kind kind[n];
+                uint8_t* p[n];
+                bool pinned_reg[n];
+                for (int i = 0; i < n; ++i) {
+                    kind[i] = static_cast<Kind>(rng() % 3);
+                    pinned_reg[i] = false;
+                    if (kind[i] == Pool) {
+                        size_t cap = 0;
+                        if (blbrs_buffer_get(S, &p[i], &cap) != BLBRS_OK) kind[i] = Pageable;  // over the limit
+                    }
+                    if (kind[i] == Registered) {
+                        p[i] = static_cast<uint8_t*>(std::aligned_alloc(4096, alloc));
+                        const int rc = blbrs_buffer_register(p[i], alloc);
+                        if (rc == BLBRS_OK) pinned_reg[i] = true;
+                        else if (rc == BLBRS_ERR_LIMIT) ++refused;
+                        else report(std::string("register: ") + blbrs_last_error());
+                    }
+                    if (kind[i] == Pageable) p[i] = static_cast<uint8_t*>(std::malloc(S));
+                }
+                int kinds_seen = 0;
+                for (int i = 0; i < n; ++i) kinds_seen |= 1 << kind[i];
+                if (__builtin_popcount(kinds_seen) > 1) ++mixed_calls;
+                std::vector<uint8_t> truth(n * S);
+                for (int i = 0; i < k; ++i)
+                    for (size_t b = 0; b < S; ++b) truth[i * S + b] = static_cast<uint8_t>(rng());
+                for (int r = k; r < n; ++r)
+                    for (int i = 0; i < k; ++i) {
+                        const uint8_t* row = gf.mul[mat[r * k + i]];
+                        for (size_t b = 0; b < S; ++b) truth[r * S + b] ^= row[truth[i * S + b]];
+                    }
+                for (int i = 0; i < k; ++i) std::memcpy(p[i], truth.data() + i * S, S);
+                for (int i = k; i < n; ++i) std::memset(p[i], 0x5A, S);
+                blbrs_encoder* enc = (it + w) % 2 ? batched : lanes;
+                const std::string where = "thread " + std::to_string(w) + " iter " + std::to_string(it) +
+                                          " S=" + std::to_string(S) + (enc == batched ? " batched" : " lanes");
+                std::vector<size_t> lens(n, S);
+                if (blbrs_encode(enc, p, lens.data()) != BLBRS_OK) report(where + ": Encode: " + blbrs_last_error());
+                for (int i = k; i < n; ++i)
+                    if (std::memcmp(p[i], truth.data() + i * S, S) != 0) report(where + ": parity " + std::to_string(i));
+                // Lose 1-3 shards, then one of Reconstruct / ReconstructData / reconstructAndVerify.
+                std::vector<int> idx(n);
+                for (int i = 0; i < n; ++i) idx[i] = i;
+                std::shuffle(idx.begin(), idx.end(), rng);
+                const int e = 1 + static_cast<int>(rng() % m);
+                for (int j = 0; j < e; ++j) {
+                    lens[idx[j]] = 0;
+                    std::memset(p[idx[j]], 0xA5, S);
+                }
+                const int op = static_cast<int>(rng() % 3);
+                // reconstructAndVerify: corrupt a present shard the decode does not read (the last
+                // present one, if it is not among the first k present) in every other call.
+                int corrupt = -1;
+                if (op == 2 && rng() % 2) {
+                    int present = 0, last = -1;
+                    for (int i = 0; i < n; ++i)
+                        if (lens[i]) { ++present; last = i; }
+                    if (present > k) {
+                        corrupt = last;
+                        p[last][S / 2] ^= 0x01;
+                    }
+                }
+                int rc, ok = 1;
+                if (op == 0) rc = blbrs_reconstruct(enc, p, lens.data());
+                else if (op == 1) rc = blbrs_reconstruct_data(enc, p, lens.data());
+                else rc = blbrs_reconstruct_verify(enc, p, lens.data(), &ok);
+                if (rc != BLBRS_OK) report(where + ": reconstruct op " + std::to_string(op) + ": " + blbrs_last_error());
+                if (op == 2 && ok != (corrupt < 0 ? 1 : 0))
+                    report(where + ": reconstructAndVerify ok=" + std::to_string(ok) + " corrupt=" + std::to_string(corrupt));
+                for (int j = 0; j < e; ++j) {
+                    const int i = idx[j];
+                    const bool want = op != 1 || i < k;
+                    if (want && std::memcmp(p[i], truth.data() + i * S, S) != 0)
+                        report(where + ": op " + std::to_string(op) + " shard " + std::to_string(i) + " wrong");
+                    if (!want && (p[i][0] != 0xA5 || p[i][S - 1] != 0xA5))
+                        report(where + ": ReconstructData touched parity " + std::to_string(i));
+                }
+                for (int i = 0; i < n; ++i) {
+                    if (kind[i] == Pool) blbrs_buffer_put(p[i]);
+                    else {
+                        if (pinned_reg[i] && blbrs_buffer_unregister(p[i]) != BLBRS_OK)
+                            report(where + ": unregister: " + blbrs_last_error());
+                        std::free(p[i]);
+                    }
+                }
+            }
+        });
+    for (auto& x : th) x.join();
+    blbrs_lane_stats l0{}, l1{};
+    blbrs_encoder_lane_stats(lanes, 0, &l0);
+    blbrs_encoder_lane_stats(lanes, 1, &l1);
+    blbrs_pool_stats ps1{};
+    blbrs_get_pool_stats(&ps1);
+    blbrs_encoder_set_batcher(batched, nullptr);
+    blbrs_batcher_free(bat);
+    blbrs_free(batched);
+    blbrs_free(lanes);
+    blbrs_pool_set_live_limit(ps0.live_limit);
+    for (const auto& s : errors) t->Errorf("%s", s.c_str());
+    if (ps1.registered_bytes != ps0.registered_bytes)
+        t->Errorf("registered bytes %llu after the test, %llu before", (unsigned long long)ps1.registered_bytes,
+                  (unsigned long long)ps0.registered_bytes);
+    if (l0.inflight_calls != 0 || l1.inflight_calls != 0) t->Errorf("lanes still report calls in flight");
+    std::printf("    lanes: %llu / %llu calls, %llu / %llu bytes; %d registrations refused by the limit; %d mixed calls\n",
+                (unsigned long long)l0.calls, (unsigned long long)l1.calls, (unsigned long long)l0.bytes,
+                (unsigned long long)l1.bytes, refused.load(), mixed_calls.load());
+}
+
 int main(int argc, char** argv) {
     const bool cpu_only = argc > 1 && std::string(argv[1]) == "--cpu";
     struct Test { const char* name; void (*fn)(T*); bool gpu; };
@@ -761,6 +926,7 @@ int main(int argc, char** argv) {
         {"TestRSEncodeStopsAtFailingWrite/pipelined", [](T* t) { TestRSEncodeStopsAtFailingWrite(t, true); }, true},
         {"TestRSEncodeConcurrentBatched", TestRSEncodeConcurrentBatched, true},
         {"TestRecoveryWriteCRC", TestRecoveryWriteCRC, true},
+        {"TestConcurrentHostSlots", TestConcurrentHostSlots, true},
     };
     int failed = 0, ran = 0;
     for (const Test& tc : tests) {

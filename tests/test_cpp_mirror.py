@@ -46,5 +46,5 @@ def test_cpp_mirror_gpu():
     out = _run(_build("_build/rs_test"))
     for name in ("TestRSEncode", "TestRSEncode/pipelined", "TestRSReconstruct", "TestRSReconstruct/pipelined",
                  "TestReconstructDataIntoCallerBuffer", "TestClientRecovery", "TestPackThenRSEncode",
-                 "TestRecoveryWriteCRC"):
+                 "TestRecoveryWriteCRC", "TestConcurrentHostSlots"):
         assert f"--- PASS: {name}\n" in out, name

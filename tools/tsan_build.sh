@@ -1,0 +1,22 @@
+#!/bin/bash
+# ThreadSanitizer build of the host runtime and the C++ mirror's tests (host code only: the
+# device code is not instrumented).  Run here, on the CPU; the GPU box only runs the result:
+#   bash tools/tsan_build.sh && gpurun -- 'bash tools/gpu_tsan.sh r3tsan'
+set -euo pipefail
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$ROOT/tools/_build/tsan
+mkdir -p "$OUT"
+pids=()
+for f in runtime rs_kernels crc32c encode_crc encode_crc_tile pack pack_encode blbrs; do
+  /opt/rocm/bin/hipcc -O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Xarch_host -fsanitize=thread \
+    -c "$ROOT/blb_amd/csrc/$f.hip" -o "$OUT/$f.o" &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait "$p"; done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -fno-gpu-sanitize -fsanitize=thread \
+  -o "$OUT/libblbrs.so" "$OUT"/*.o
+rm -f "$OUT"/*.o
+/opt/rocm/llvm/bin/clang++ -O1 -g -std=c++17 -pthread -fsanitize=thread -o "$OUT/rs_test_tsan" \
+  "$ROOT/tests/cpp/rs_test.cpp" "$ROOT"/blb_amd/host/{reedsolomon,tractserver,client}.cpp \
+  -L"$OUT" -lblbrs -Wl,-rpath,'$ORIGIN' -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+ls -la "$OUT"
