@@ -20,6 +20,7 @@ SIGNATURES = {
     "blbrs_data_shards": (_I, [_P]),
     "blbrs_parity_shards": (_I, [_P]),
     "blbrs_matrix": (_I, [_P, _P, _SZ]),
+    "blbrs_encoder_compiled_network": (_I, [_P]),
     "blbrs_encode": (_I, [_P, _P, _P]),
     "blbrs_verify": (_I, [_P, _P, _P, ctypes.POINTER(_I)]),
     "blbrs_reconstruct": (_I, [_P, _P, _P]),

@@ -36,6 +36,7 @@
 #include "crc32c.hpp"
 #include "encode_crc.hpp"
 #include "gf256.hpp"
+#include "gf_bitslice.hpp"
 #include "pack.hpp"
 #include "rs_kernels.hpp"
 #include "runtime.hpp"
@@ -58,6 +59,7 @@ namespace {
 struct Pass {
     int k_in = 0, rows = 0;
     int nstore = -1;  // store+verify plans: rows [0, nstore) of this pass are stored
+    bool parity = false;  // rows = encode parity rows 0..rows-1 of k_in (compiled network)
     std::vector<int32_t> in_idx, out_idx;
     std::vector<uint32_t> tables;
 };
@@ -85,6 +87,7 @@ void split_passes(HostPlan& p) {
         Mat sub(p.rows.begin() + static_cast<size_t>(r0) * p.k_in,
                 p.rows.begin() + static_cast<size_t>(r0 + ps.rows) * p.k_in);
         ps.tables = perm_tables(sub, ps.rows, p.k_in);
+        ps.parity = bs::is_parity_rows(sub.data(), ps.rows, p.k_in);
         p.passes.push_back(std::move(ps));
     }
 }
@@ -97,6 +100,7 @@ struct DevPass {
     const uint32_t* tables = nullptr;
     int k_in = 0, rows = 0;
     int nstore = -1;
+    bool parity = false;
 };
 struct DevPlan {
     std::vector<DevPass> passes;
@@ -118,6 +122,7 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
         d.k_in = ps.k_in;
         d.rows = ps.rows;
         d.nstore = ps.nstore;
+        d.parity = ps.parity;
         const size_t n_in = ps.in_idx.size() * 4, n_out = round_up(ps.out_idx.size() * 4, 16);
         const size_t off_out = round_up(n_in, 16), off_tab = off_out + n_out;
         const size_t bytes = off_tab + ps.tables.size() * 4;
@@ -365,6 +370,7 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         a.rows = ps.rows;
         a.aligned = st.aligned ? 1 : 0;
         a.mismatch = mismatch;
+        a.parity = ps.parity ? 1 : 0;
         Mode m = mode;
         if (mode == Mode::kStoreVerify) {  // per pass: all stored, all compared, or mixed
             a.nstore = ps.nstore;
@@ -1053,6 +1059,14 @@ void blbrs_free(blbrs_encoder* enc) { delete enc; }
 int blbrs_data_shards(const blbrs_encoder* enc) { return enc ? enc->k : 0; }
 int blbrs_parity_shards(const blbrs_encoder* enc) { return enc ? enc->m : 0; }
 
+int blbrs_encoder_compiled_network(const blbrs_encoder* enc) {
+    if (!enc || !bs::enabled()) return 0;
+    const auto hp = enc->core->encode_plan();
+    for (const Pass& ps : hp->passes)
+        if (!ps.parity) return 0;
+    return 1;
+}
+
 int blbrs_matrix(const blbrs_encoder* enc, uint8_t* out, size_t cap) {
     if (!enc || !out) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     const Mat& mat = enc->core->matrix;
@@ -1513,6 +1527,7 @@ static int code_crc_dev(blbrs_encoder* enc, const std::string& key, const HostPl
         a.crc = crc_out_dev;
         a.phase = phase;
         a.seeds = seeds_dev;
+        a.parity = ps.parity;
         if (encode_crc_supported(a)) {
             const hipError_t e = launch_encode_crc(a, s);
             if (e != hipSuccess) return hip_fail(e, "launch encode_crc_kernel");

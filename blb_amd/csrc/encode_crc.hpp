@@ -21,6 +21,7 @@ struct EncodeCrcArgs {
     uint32_t* crc;            // device: [rows][B][nblocks], nblocks = ceil((phase + S) / block)
     uint64_t phase = 0;       // file offset of byte 0 of each shard, mod block (< block)
     const uint32_t* seeds = nullptr;  // device [rows][B]: crc32.Update seed of block 0, or NULL
+    bool parity = false;      // rows are encode parity rows 0..rows-1 of k (gf_bitslice.hpp)
 };
 
 // True when a fused kernel covers this shape: the tile-grid kernel (below), or the segment

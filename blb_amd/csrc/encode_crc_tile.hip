@@ -36,6 +36,7 @@
 #include <mutex>
 
 #include "crc_device.hpp"
+#include "gf_bitslice.hpp"
 #include "gf_device.hpp"
 
 namespace blbrs {
@@ -362,14 +363,30 @@ __device__ __forceinline__ void load_tile(const TArgs& a, const uint8_t* stripe,
     }
 }
 
-// The parity rows of the tile (v_perm multiply), stored nontemporal; acc keeps them.
-template <int K, int MR, int LC, bool PARTIAL>
+// Parity rows R.. of the compiled encode network (gf_bitslice.hpp) from the input planes.
+template <int K, int MR, int R>
+__device__ __forceinline__ void bs_rows(const uint32_t (&x)[K][8], uint32_t (&acc)[MR][8]) {
+    if constexpr (R < MR) {
+        bs::parity_row<K, R>(x, acc[R]);
+        bs_rows<K, MR, R + 1>(x, acc);
+    }
+}
+
+// The parity rows of the tile, stored nontemporal; acc keeps them.  CM: the plan's rows are
+// encode parity rows 0..MR-1 of K, computed by the compiled bit-plane XOR network (the
+// inputs are transposed in place); otherwise the v_perm multiply with the plan's tables.
+template <int K, int MR, int LC, bool PARTIAL, bool CM>
 __device__ __forceinline__ void code_tile(const TArgs& a, uint8_t* stripe, uint64_t tile_off, uint32_t in_tile,
                                           uint32_t lim, uint32_t (&x)[K][LC / 4], uint32_t (&acc)[MR][LC / 4]) {
     constexpr int NV = LC / 4;
     constexpr int NQ = LC / 16;
     const ci32 out_idx = as_const(a.out_idx);
-    {
+    if constexpr (CM) {
+        static_assert(NV == 8, "bit planes of 8 dwords");
+#pragma unroll
+        for (int c = 0; c < K; ++c) bs::transpose8(x[c]);
+        bs_rows<K, MR, 0>(x, acc);
+    } else {
         cu32 tables = as_const(a.tables);
         asm volatile("" : "+s"(tables));
 #pragma unroll
@@ -399,7 +416,7 @@ __device__ __forceinline__ void code_tile(const TArgs& a, uint8_t* stripe, uint6
 // tile's CRC) held 149-197 VGPRs and lost 5-7 % (r2g).
 // Wide-slicing builds hold the main instantiations to 3 waves per SIMD (RS(12,5) lands one
 // VGPR past 168 otherwise); the partial-tile launch (B workgroups) is left unconstrained.
-template <int K, int MR, int LC, bool PARTIAL>
+template <int K, int MR, int LC, bool PARTIAL, bool CM>
 __global__ __launch_bounds__(kTThreads) __attribute__((amdgpu_waves_per_eu((PARTIAL || kSlice == 8) ? 1 : 3)))
 void encode_crc_tile_kernel(TArgs a) {
     constexpr int NV = LC / 4;
@@ -467,7 +484,7 @@ void encode_crc_tile_kernel(TArgs a) {
     if (tid < 96u) wm[tid] = wmv;
 
     uint32_t acc[MR][NV] = {};
-    code_tile<K, MR, LC, PARTIAL>(a, stripe, tile_off, in_tile, lim, x, acc);
+    code_tile<K, MR, LC, PARTIAL, CM>(a, stripe, tile_off, in_tile, lim, x, acc);
     // CRC of this lane's LC contiguous parity bytes (tile offset LC * tid) per row.
 #pragma unroll
     for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
@@ -512,7 +529,7 @@ void encode_crc_tile_persist_kernel(TArgs a) {
         uint32_t x[K][NV];
         load_tile<K, LC, false>(a, stripe, tile_off, in_tile, kTile, x);
         uint32_t acc[MR][NV] = {};
-        code_tile<K, MR, LC, false>(a, stripe, tile_off, in_tile, kTile, x, acc);
+        code_tile<K, MR, LC, false, false>(a, stripe, tile_off, in_tile, kTile, x, acc);
 #pragma unroll
         for (int j = 0; j < MR; ++j) lane_contiguous<LC>(acc[j]);
         crc_tile<MR, LC>(a, acc, tab, nib, wm, red[it & 1u], tile_off, static_cast<uint64_t>(b) * a.tps + tile, tid,
@@ -607,27 +624,37 @@ __global__ __launch_bounds__(256) void tile_combine_kernel(TArgs a, uint32_t log
 
 using KernelFn = void (*)(TArgs);
 
+template <int K, int MR, bool P>
+KernelFn pick_cm(bool cm) {
+    constexpr int LC = lc_for(K, MR);
+    if constexpr (LC == 32) {
+        if (cm) return encode_crc_tile_kernel<K, MR, LC, P, true>;
+    }
+    return encode_crc_tile_kernel<K, MR, LC, P, false>;
+}
+
 template <int K, bool P>
-KernelFn pick_rows(int rows) {
+KernelFn pick_rows(int rows, bool cm) {
     switch (rows) {
-        case 1: return encode_crc_tile_kernel<K, 1, lc_for(K, 1), P>;
-        case 2: return encode_crc_tile_kernel<K, 2, lc_for(K, 2), P>;
-        case 3: return encode_crc_tile_kernel<K, 3, lc_for(K, 3), P>;
-        case 4: return encode_crc_tile_kernel<K, 4, lc_for(K, 4), P>;
-        case 5: return encode_crc_tile_kernel<K, 5, lc_for(K, 5), P>;
+        case 1: return pick_cm<K, 1, P>(cm);
+        case 2: return pick_cm<K, 2, P>(cm);
+        case 3: return pick_cm<K, 3, P>(cm);
+        case 4: return pick_cm<K, 4, P>(cm);
+        case 5: return pick_cm<K, 5, P>(cm);
         default: return nullptr;
     }
 }
 
 // Same instantiated shapes as encode_crc.hip (blb's classes, RS(10,4), RS(3,2), RS(4,2)).
-KernelFn pick(int k, int rows, bool partial = false) {
+// cm: the pass computes encode parity rows (the compiled bit-plane network).
+KernelFn pick(int k, int rows, bool partial = false, bool cm = false) {
     switch (k) {
-        case 3: return partial ? pick_rows<3, true>(rows) : pick_rows<3, false>(rows);
-        case 4: return partial ? pick_rows<4, true>(rows) : pick_rows<4, false>(rows);
-        case 6: return partial ? pick_rows<6, true>(rows) : pick_rows<6, false>(rows);
-        case 8: return partial ? pick_rows<8, true>(rows) : pick_rows<8, false>(rows);
-        case 10: return partial ? pick_rows<10, true>(rows) : pick_rows<10, false>(rows);
-        case 12: return partial ? pick_rows<12, true>(rows) : pick_rows<12, false>(rows);
+        case 3: return partial ? pick_rows<3, true>(rows, cm) : pick_rows<3, false>(rows, cm);
+        case 4: return partial ? pick_rows<4, true>(rows, cm) : pick_rows<4, false>(rows, cm);
+        case 6: return partial ? pick_rows<6, true>(rows, cm) : pick_rows<6, false>(rows, cm);
+        case 8: return partial ? pick_rows<8, true>(rows, cm) : pick_rows<8, false>(rows, cm);
+        case 10: return partial ? pick_rows<10, true>(rows, cm) : pick_rows<10, false>(rows, cm);
+        case 12: return partial ? pick_rows<12, true>(rows, cm) : pick_rows<12, false>(rows, cm);
         default: return nullptr;
     }
 }
@@ -738,7 +765,8 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     if (in.B == 0 || in.S == 0) return hipSuccess;
     if (!encode_crc_tile_supported(in) || !in.crc) return hipErrorInvalidValue;
     const int lc = lc_for(in.k, in.rows);
-    const KernelFn fn = pick(in.k, in.rows);
+    const bool cm = in.parity && bs::enabled();
+    const KernelFn fn = pick(in.k, in.rows, false, cm);
     const CrcConsts* c = nullptr;
     hipError_t e = crc_consts_for(65536, &c);  // tables + pow2 (the segment size is irrelevant here)
     if (e != hipSuccess) return e;
@@ -783,11 +811,13 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
             hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), 0, stream, a);
     }
 #else
-    if (groups) hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), 0, stream, a);
+    unsigned occ = 0;  // A/B knob, as rs_kernels.hip: dynamic LDS per workgroup of the network launches
+    if (const char* v = cm ? getenv("BLBRS_OCC_LDS_ECT") : nullptr) occ = static_cast<unsigned>(std::min(atol(v), 65536L));
+    if (groups) hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), occ, stream, a);
 #endif
     e = hipGetLastError();
     if (e == hipSuccess && a.tps != a.tps_full) {
-        hipLaunchKernelGGL(pick(in.k, in.rows, true), dim3(in.B), dim3(kTThreads), 0, stream, a);
+        hipLaunchKernelGGL(pick(in.k, in.rows, true, cm), dim3(in.B), dim3(kTThreads), 0, stream, a);
         e = hipGetLastError();
     }
     const uint64_t total = static_cast<uint64_t>(in.rows) * in.B * a.nblocks;

@@ -1,0 +1,210 @@
+// gf_bitslice.hpp -- GF(2^8) encode with the coding matrix known at compile time: bit planes
+// and a fixed XOR network instead of v_perm table lookups.
+//
+// Multiplying a byte by a constant c is GF(2)-linear: bit p of c*x is the XOR of the bits q
+// of x for which bit p of c*2^q is set (an 8x8 bit matrix per coefficient).  Encode's
+// coefficients are the parity rows P_j = V[k+j] * inv(V[0:k]) of reedsolomon.go buildMatrix
+// (klauspost @925cb01d6510), fixed per k -- and independent of m, since V's rows do not
+// depend on it -- so for blb's shapes the whole row of bit matrices is known when the kernel
+// is compiled.  Then:
+//   * 8 dwords of a shard (32 bytes per lane) are bit-transposed in place (transpose8: byte
+//     lane b of dword i <-> bit i of byte lane b, three SWAR stages, 4 VALU per dword pair
+//     per stage = 6 VALU per dword), so dword q holds bit q of all 32 bytes -- a "plane";
+//   * parity plane (j, p) = XOR of the input planes (c, q) with bit p of P_j[c]*2^q set,
+//     a fixed list of terms folded three at a time with v_bitop3 (XOR3); no table operand, no
+//     constant-bus move, no bit-group split;
+//   * the 8 parity planes of a row are transposed back (the transpose is an involution).
+// VALU per 4 bytes of every shard (one dword column): RS(6,3) 81 vs 115 with v_perm tables,
+// RS(10,4) 159 vs 240, RS(12,5) 211 vs 345 (tools/bitslice_count.py).  Decode matrices
+// depend on the erasure pattern and stay on the v_perm path (gf_device.hpp).
+#pragma once
+#include <cstdint>
+#include <cstdlib>
+
+#include "dev_common.hpp"
+
+namespace blbrs {
+namespace bs {
+
+constexpr int kMaxParity = 5;  // parity rows compiled per k (blb's classes need m <= 5)
+
+// --- compile-time field and parity rows (same construction as gf256.hpp, constexpr) -------
+struct CField {
+    uint8_t exp[512] = {};
+    uint8_t log[256] = {};
+};
+constexpr CField make_field() {
+    CField f{};
+    unsigned x = 1;
+    for (int i = 0; i < 255; ++i) {
+        f.exp[i] = f.exp[i + 255] = static_cast<uint8_t>(x);
+        f.log[x] = static_cast<uint8_t>(i);
+        x <<= 1;
+        if (x & 0x100) x ^= 0x11d;
+    }
+    f.exp[510] = f.exp[511] = f.exp[0];
+    return f;
+}
+constexpr CField kField = make_field();
+constexpr uint8_t cmul(uint8_t a, uint8_t b) {
+    return (a == 0 || b == 0) ? 0 : kField.exp[kField.log[a] + kField.log[b]];
+}
+constexpr uint8_t cinv(uint8_t a) { return kField.exp[(255 - kField.log[a]) % 255]; }
+constexpr uint8_t cpow(uint8_t a, int n) {
+    return n == 0 ? 1 : a == 0 ? 0 : kField.exp[(static_cast<int>(kField.log[a]) * n) % 255];
+}
+
+template <int K>
+struct ParityRows {
+    uint8_t c[kMaxParity][K] = {};
+};
+
+// P_j = V[K+j] * inv(V[0:K]), V[r][c] = r^c (matrix.go vandermonde, reedsolomon.go buildMatrix).
+template <int K>
+constexpr ParityRows<K> make_parity_rows() {
+    uint8_t t[K][2 * K] = {};
+    for (int r = 0; r < K; ++r) {
+        for (int c = 0; c < K; ++c) t[r][c] = cpow(static_cast<uint8_t>(r), c);
+        t[r][K + r] = 1;
+    }
+    for (int col = 0; col < K; ++col) {  // Gauss-Jordan, as gf256.hpp invert()
+        int piv = col;
+        while (t[piv][col] == 0) ++piv;  // V[0:K] is invertible
+        if (piv != col)
+            for (int j = 0; j < 2 * K; ++j) {
+                const uint8_t s = t[col][j];
+                t[col][j] = t[piv][j];
+                t[piv][j] = s;
+            }
+        const uint8_t s = cinv(t[col][col]);
+        for (int j = 0; j < 2 * K; ++j) t[col][j] = cmul(t[col][j], s);
+        for (int r = 0; r < K; ++r) {
+            const uint8_t f = t[r][col];
+            if (r == col || f == 0) continue;
+            for (int j = 0; j < 2 * K; ++j) t[r][j] ^= cmul(f, t[col][j]);
+        }
+    }
+    ParityRows<K> p{};
+    for (int j = 0; j < kMaxParity; ++j)
+        for (int c = 0; c < K; ++c) {
+            uint8_t v = 0;
+            for (int i = 0; i < K; ++i) v ^= cmul(cpow(static_cast<uint8_t>(K + j), i), t[i][K + c]);
+            p.c[j][c] = v;
+        }
+    return p;
+}
+
+template <int K>
+constexpr ParityRows<K> kParity = make_parity_rows<K>();
+
+// The XOR network: for parity row j and output bit p, the input planes (c, q) to fold.
+template <int K>
+struct Terms {
+    int n[kMaxParity][8] = {};
+    uint8_t c[kMaxParity][8][8 * K] = {};
+    uint8_t q[kMaxParity][8][8 * K] = {};
+};
+template <int K>
+constexpr Terms<K> make_terms() {
+    Terms<K> t{};
+    for (int j = 0; j < kMaxParity; ++j)
+        for (int c = 0; c < K; ++c)
+            for (int q = 0; q < 8; ++q) {
+                const uint8_t col = cmul(kParity<K>.c[j][c], static_cast<uint8_t>(1u << q));
+                for (int p = 0; p < 8; ++p)
+                    if ((col >> p) & 1u) {
+                        const int i = t.n[j][p]++;
+                        t.c[j][p][i] = static_cast<uint8_t>(c);
+                        t.q[j][p][i] = static_cast<uint8_t>(q);
+                    }
+            }
+    return t;
+}
+template <int K>
+constexpr Terms<K> kTerms = make_terms<K>();
+
+// Host side: true when `rows` (nrows x k, row-major) are parity rows 0..nrows-1 of k, i.e.
+// a pass the compiled network computes.
+template <int K>
+bool is_parity_rows_k(const uint8_t* rows, int nrows) {
+    if (nrows < 1 || nrows > kMaxParity) return false;
+    for (int j = 0; j < nrows; ++j)
+        for (int c = 0; c < K; ++c)
+            if (rows[j * K + c] != kParity<K>.c[j][c]) return false;
+    return true;
+}
+inline bool is_parity_rows(const uint8_t* rows, int nrows, int k) {
+    switch (k) {
+        case 3: return is_parity_rows_k<3>(rows, nrows);
+        case 4: return is_parity_rows_k<4>(rows, nrows);
+        case 6: return is_parity_rows_k<6>(rows, nrows);
+        case 8: return is_parity_rows_k<8>(rows, nrows);
+        case 10: return is_parity_rows_k<10>(rows, nrows);
+        case 12: return is_parity_rows_k<12>(rows, nrows);
+        default: return false;
+    }
+}
+
+// BLBRS_BITSLICE=0, read per launch, runs encode passes on the v_perm path (A/B runs).
+inline bool enabled() {
+    const char* e = getenv("BLBRS_BITSLICE");
+    return !(e && e[0] == '0');
+}
+
+// --- device ----------------------------------------------------------------------------
+
+// 8x8 bit transpose inside every byte lane of 8 dwords: afterwards bit i of byte b of d[q]
+// is what bit q of byte b of d[i] was.  Stage s swaps element (i, q + s) with (i + s, q) for
+// q with bit s clear; v_bfi_b32 merges, so each pair costs 2 shifts + 2 bfi.
+template <int S>
+__device__ __forceinline__ void transpose_stage(uint32_t* d) {
+    constexpr uint32_t m = S == 4 ? 0x0F0F0F0Fu : S == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int i = (h / S) * 2 * S + h % S;  // the four rows with bit S clear
+        const uint32_t a = d[i], b = d[i + S];
+        d[i] = (a & m) | ((b << S) & ~m);
+        d[i + S] = ((a >> S) & m) | (b & ~m);
+    }
+}
+__device__ __forceinline__ void transpose8(uint32_t* d) {
+    transpose_stage<4>(d);
+    transpose_stage<2>(d);
+    transpose_stage<1>(d);
+}
+
+// XOR of terms [J, n) of parity row R, output bit P, three at a time.
+template <int K, int R, int P, int J>
+__device__ __forceinline__ uint32_t fold(const uint32_t (&x)[K][8]) {
+    constexpr int n = kTerms<K>.n[R][P];
+    if constexpr (J >= n) {
+        return 0u;
+    } else if constexpr (J + 1 == n) {
+        return x[kTerms<K>.c[R][P][J]][kTerms<K>.q[R][P][J]];
+    } else if constexpr (J + 2 == n) {
+        return x[kTerms<K>.c[R][P][J]][kTerms<K>.q[R][P][J]] ^ x[kTerms<K>.c[R][P][J + 1]][kTerms<K>.q[R][P][J + 1]];
+    } else {
+        return dev::xor3(x[kTerms<K>.c[R][P][J]][kTerms<K>.q[R][P][J]],
+                         x[kTerms<K>.c[R][P][J + 1]][kTerms<K>.q[R][P][J + 1]], fold<K, R, P, J + 2>(x));
+    }
+}
+
+template <int K, int R, int P>
+__device__ __forceinline__ void row_planes(const uint32_t (&x)[K][8], uint32_t* out) {
+    if constexpr (P < 8) {
+        out[P] = fold<K, R, P, 0>(x);
+        row_planes<K, R, P + 1>(x, out);
+    }
+}
+
+// Parity row R of 8 dwords per input: x holds the K inputs' planes (transposed in place by
+// the caller), out gets the row's 8 dwords in byte form.
+template <int K, int R>
+__device__ __forceinline__ void parity_row(const uint32_t (&x)[K][8], uint32_t* out) {
+    static_assert(R < kMaxParity, "parity row");
+    row_planes<K, R, 0>(x, out);
+    transpose8(out);
+}
+
+}  // namespace bs
+}  // namespace blbrs

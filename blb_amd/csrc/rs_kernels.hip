@@ -32,6 +32,7 @@
 
 #include <algorithm>
 
+#include "gf_bitslice.hpp"
 #include "gf_device.hpp"
 
 namespace blbrs {
@@ -124,14 +125,26 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
     }
 }
 
+// Parity rows R.. of the compiled encode network over one 8-dword group of every input.
+template <int K, int MR, int R>
+__device__ __forceinline__ void bs_rows(const uint32_t (&xs)[K][8], uint32_t (&acc)[MR][8]) {
+    if constexpr (R < MR) {
+        bs::parity_row<K, R>(xs, acc[R]);
+        bs_rows<K, MR, R + 1>(xs, acc);
+    }
+}
+
 // K > 0: compile-time input count (all K*U chunk loads issued before any math).
 // K == 0: runtime k (loads issued per input, two inputs unrolled).
 // MR: compile-time bound on output rows; a.rows <= MR honoured at runtime.
 // MODE 0 = store outputs, 1 = compare against existing outputs (Verify), 2 = store rows
 // [0, a.nstore) and compare the rest (reconstructAndVerify in one pass).
 // ADDR 0 = strided stripes, 1 = pointer table.  U = 16-byte chunks per lane per tile.
-template <int K, int MR, int MODE, int ADDR, int U, int NT>
+// CM: the rows are encode parity rows 0..MR-1 of K (a.rows == MR), computed by the compiled
+// bit-plane XOR network of gf_bitslice.hpp on whole tiles (K > 0, U even).
+template <int K, int MR, int MODE, int ADDR, int U, int NT, bool CM = false>
 __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
+    static_assert(!CM || (K > 0 && U % 2 == 0 && MODE != 2), "compiled network shapes");
     constexpr uint32_t kTile = kTileBytes * U;
     const uint32_t total = a.B * a.tiles_per_stripe;
     const int nr = a.rows;
@@ -183,6 +196,23 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) x[c][u] = ld16<NT>(p + u * kStep);
             }
+            if constexpr (CM) {
+#pragma unroll
+                for (int g = 0; g < U / 2; ++g) {
+                    uint32_t xs[K][8], og[MR][8];
+#pragma unroll
+                    for (int c = 0; c < K; ++c) {
+                        unpack(x[c][2 * g], xs[c]);
+                        unpack(x[c][2 * g + 1], xs[c] + 4);
+                        bs::transpose8(xs[c]);
+                    }
+                    bs_rows<K, MR, 0>(xs, og);
+#pragma unroll
+                    for (int r = 0; r < MR; ++r)
+#pragma unroll
+                        for (int d = 0; d < 8; ++d) acc[r][8 * g + d] = og[r][d];
+                }
+            } else {
 #pragma unroll
             for (int c = 0; c + 1 < K; c += 2) {
                 uint32_t xa[NV], xb[NV];
@@ -196,6 +226,7 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) unpack(x[K - 1][u], xv + 4 * u);
                 madd<MR, NV>(Groups<NV>(xv), [&](int r) { return tables + (r * K + K - 1) * 5; }, acc, nr);
+            }
             }
         } else {
             const int k = a.k;
@@ -276,16 +307,27 @@ struct Choice {
     KernelFn fn = nullptr;
     int u = 0;
     bool fixed = false;
+    bool cm = false;  // the compiled encode network
 };
 
+// Encode / Verify passes of parity rows: the compiled network where the shape has one.
+template <int K, int MR, int MODE, int ADDR>
+Choice choice_of(bool cm) {
+    constexpr int U = pick_u(K, MR, MODE);
+    if constexpr (K > 0 && U % 2 == 0 && MODE != 2) {
+        if (cm) return {rs_code_kernel<K, MR, MODE, ADDR, U, kNT, true>, U, true, true};
+    }
+    return {fn_of<K, MR, MODE, ADDR>(), U, K > 0, false};
+}
+
 template <int K, int MODE, int ADDR>
-Choice pick_rows(int rows) {
+Choice pick_rows(int rows, bool cm = false) {
     switch (rows) {
-        case 1: return {fn_of<K, 1, MODE, ADDR>(), pick_u(K, 1, MODE), K > 0};
-        case 2: return {fn_of<K, 2, MODE, ADDR>(), pick_u(K, 2, MODE), K > 0};
-        case 3: return {fn_of<K, 3, MODE, ADDR>(), pick_u(K, 3, MODE), K > 0};
-        case 4: return {fn_of<K, 4, MODE, ADDR>(), pick_u(K, 4, MODE), K > 0};
-        case 5: return {fn_of<K, 5, MODE, ADDR>(), pick_u(K, 5, MODE), K > 0};
+        case 1: return choice_of<K, 1, MODE, ADDR>(cm);
+        case 2: return choice_of<K, 2, MODE, ADDR>(cm);
+        case 3: return choice_of<K, 3, MODE, ADDR>(cm);
+        case 4: return choice_of<K, 4, MODE, ADDR>(cm);
+        case 5: return choice_of<K, 5, MODE, ADDR>(cm);
         case 6: return {fn_of<0, 6, MODE, ADDR>(), pick_u(0, 6, MODE), false};
         case 7: return {fn_of<0, 7, MODE, ADDR>(), pick_u(0, 7, MODE), false};
         case 8: return {fn_of<0, 8, MODE, ADDR>(), pick_u(0, 8, MODE), false};
@@ -294,10 +336,10 @@ Choice pick_rows(int rows) {
 }
 
 template <int MODE, int ADDR>
-Choice pick_k(int k, int rows) {
+Choice pick_k(int k, int rows, bool cm) {
     if (rows <= kMaxTemplRows) {
         switch (k) {
-#define BLBRS_CASE(KK) case KK: return pick_rows<KK, MODE, ADDR>(rows);
+#define BLBRS_CASE(KK) case KK: return pick_rows<KK, MODE, ADDR>(rows, cm);
             BLBRS_K_LIST(BLBRS_CASE)
 #undef BLBRS_CASE
             default: break;
@@ -306,10 +348,19 @@ Choice pick_k(int k, int rows) {
     return pick_rows<0, MODE, ADDR>(rows);
 }
 
-Choice pick(int k, int rows, Mode mode, bool strided) {
-    if (mode == Mode::kStore) return strided ? pick_k<0, 0>(k, rows) : pick_k<0, 1>(k, rows);
-    if (mode == Mode::kVerify) return strided ? pick_k<1, 0>(k, rows) : pick_k<1, 1>(k, rows);
-    return strided ? pick_k<2, 0>(k, rows) : pick_k<2, 1>(k, rows);
+Choice pick(int k, int rows, Mode mode, bool strided, bool cm = false) {
+    if (mode == Mode::kStore) return strided ? pick_k<0, 0>(k, rows, cm) : pick_k<0, 1>(k, rows, cm);
+    if (mode == Mode::kVerify) return strided ? pick_k<1, 0>(k, rows, cm) : pick_k<1, 1>(k, rows, cm);
+    return strided ? pick_k<2, 0>(k, rows, false) : pick_k<2, 1>(k, rows, false);
+}
+
+// A/B knob: BLBRS_OCC_LDS=<bytes> (<= 64 KiB, read per launch) reserves that much dynamic LDS
+// per workgroup of the compiled-network launches, capping workgroups per CU (160 KiB / bytes).
+unsigned occupancy_lds(bool cm) {
+    if (!cm) return 0;
+    const char* e = getenv("BLBRS_OCC_LDS");
+    const long v = e ? atol(e) : 0;
+    return v > 0 && v <= 65536 ? static_cast<unsigned>(v) : 0u;
 }
 
 }  // namespace
@@ -319,7 +370,7 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream) {
     if (mode != Mode::kStore && !args.mismatch) return hipErrorInvalidValue;
     if (mode == Mode::kStoreVerify && (args.nstore < 0 || args.nstore > args.rows)) return hipErrorInvalidValue;
     if (args.B == 0 || args.S == 0) return hipSuccess;
-    const Choice ch = pick(args.k, args.rows, mode, args.base != nullptr);
+    const Choice ch = pick(args.k, args.rows, mode, args.base != nullptr, args.parity && bs::enabled());
     if (!ch.fn) return hipErrorInvalidValue;
     const uint64_t tile = static_cast<uint64_t>(kTileBytes) * ch.u;
     const uint64_t tps = (args.S + tile - 1) / tile;
@@ -339,16 +390,18 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream) {
             grid = total & ~uint64_t{7};
             a.xcd_remap = 1;
         }
-        hipLaunchKernelGGL(ch.fn, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream, a);
+        hipLaunchKernelGGL(ch.fn, dim3(static_cast<unsigned>(grid)), dim3(kThreads), occupancy_lds(ch.cm), stream, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
 
-const char* kernel_name(int k, int rows, Mode mode) {
-    const Choice ch = pick(k, rows, mode, true);
-    return ch.fixed ? "rs_code_kernel<K,MR,MODE,ADDR,U,NT>" : "rs_code_kernel<0,MR,MODE,ADDR,U,NT>";
+const char* kernel_name(int k, int rows, Mode mode, bool parity) {
+    const Choice ch = pick(k, rows, mode, true, parity && bs::enabled());
+    return ch.cm      ? "rs_code_kernel<K,MR,MODE,ADDR,U,NT,true>"
+           : ch.fixed ? "rs_code_kernel<K,MR,MODE,ADDR,U,NT>"
+                      : "rs_code_kernel<0,MR,MODE,ADDR,U,NT>";
 }
 
 }  // namespace blbrs

@@ -27,6 +27,8 @@ struct CodeArgs {
     int32_t* mismatch;        // verify: [B] flags (device)
     int32_t xcd_remap;        // set by launch_code(): block b starts at tile (b%8)*(grid/8) + b/8
     int32_t nstore;           // kStoreVerify: rows [0, nstore) are stored, the rest compared
+    int32_t parity;           // rows = encode parity rows 0..rows-1 of k: the compiled network
+                              //   (gf_bitslice.hpp) where the shape has one
 };
 
 constexpr int kThreads = 256;
@@ -44,7 +46,7 @@ enum class Mode : int { kStore = 0, kVerify = 1, kStoreVerify = 2 };
 hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream);
 
 // Name of the kernel instantiation launch_code() would pick (for profiling/tests).
-const char* kernel_name(int k, int rows, Mode mode);
+const char* kernel_name(int k, int rows, Mode mode, bool parity = false);
 
 
 }  // namespace blbrs

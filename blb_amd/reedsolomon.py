@@ -165,6 +165,11 @@ class Encoder:
         _check(self._lib.blbrs_matrix(self._h, out.ctypes.data, out.size))
         return out
 
+    def compiled_network(self) -> bool:
+        """True when Encode / Verify run the compiled bit-plane network for this (k, m)
+        (blbrs_encoder_compiled_network); False on the v_perm table path."""
+        return bool(self._lib.blbrs_encoder_compiled_network(self._h))
+
     # ---- helpers ----
     def _arrays(self, shards, n):
         ptrs = (ctypes.c_void_p * n)()

@@ -106,3 +106,17 @@ def test_c_abi_null_arguments():
     lib.blbrs_free(h)
     assert lib.blbrs_strerror(-3).decode() == "too few shards given"
     assert b"gfx950" in lib.blbrs_version()
+
+
+def test_compiled_network_covers_blb_classes(monkeypatch):
+    """The parity rows built into the library (gf_bitslice.hpp, constexpr buildMatrix) equal
+    the runtime matrix for every compiled (k, m): Encode / Verify of those shapes run the
+    bit-plane network.  Other shapes, and BLBRS_BITSLICE=0, keep the v_perm table path."""
+    from blb_amd import reedsolomon as rs
+    for k in (3, 4, 6, 8, 10, 12):
+        for m in range(1, 6):
+            assert rs.New(k, m).compiled_network(), (k, m)
+    for k, m in ((5, 3), (10, 6), (2, 2), (20, 4)):
+        assert not rs.New(k, m).compiled_network(), (k, m)
+    monkeypatch.setenv("BLBRS_BITSLICE", "0")
+    assert not rs.New(6, 3).compiled_network()

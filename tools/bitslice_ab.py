@@ -1,0 +1,70 @@
+"""A/B of the compiled bit-plane encode network (gf_bitslice.hpp) against the v_perm table
+path, in one process: BLBRS_BITSLICE=1 / 0 is read per launch, so the two alternate rep by
+rep on the same device buffers.  Per shape: EncodeBatch, VerifyBatch and EncodeBatchCRC on
+65532-byte blocks (ms per call, HIP events), B stripes of 8 MiB."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from blb_amd import reedsolomon as rs  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--shapes", default="6,3,1024;8,3,512;10,4,512;12,5,512")
+p.add_argument("--reps", type=int, default=3)
+p.add_argument("--iters", type=int, default=5)
+p.add_argument("--ops", default="encode,verify,encode_crc")
+# name:VAR=v+VAR2=w;... -- environment of each variant (read per launch by the library)
+p.add_argument("--variants", default="net:BLBRS_BITSLICE=1;perm:BLBRS_BITSLICE=0")
+a = p.parse_args()
+dev = torch.device("cuda:0")
+S = 8 << 20
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize(dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(a.iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize(dev)
+    return s.elapsed_time(e) / a.iters
+
+
+for spec in a.shapes.split(";"):
+    k, m, B = (int(v) for v in spec.split(","))
+    stripes = torch.randint(0, 256, (B, k + m, S), dtype=torch.uint8, device=dev)
+    enc = rs.New(k, m)
+    ops = {"encode": lambda: enc.EncodeBatch(stripes),
+           "verify": lambda: enc.VerifyBatch(stripes),
+           "encode_crc": lambda: enc.EncodeBatchCRC(stripes, 65532)}
+    variants = []
+    for v in a.variants.split(";"):
+        vname, _, envs = v.partition(":")
+        variants.append((vname, dict(kv.split("=", 1) for kv in envs.split("+") if kv)))
+    res = {}
+    for rep in range(a.reps):
+        for vname, env in variants:
+            os.environ.update(env)
+            for name in a.ops.split(","):
+                res.setdefault(f"{name}_{vname}", []).append(round(timed(ops[name]), 3))
+            for key in env:
+                os.environ.pop(key, None)
+    # the two paths write the same parity
+    enc.EncodeBatch(stripes)
+    ok = bool(enc.VerifyBatch(stripes).all())
+    os.environ["BLBRS_BITSLICE"] = "0"
+    ok_perm = bool(enc.VerifyBatch(stripes).all())
+    os.environ.pop("BLBRS_BITSLICE", None)
+    gb = B * (k + m) * S / 1e9
+    best = {key: min(v) for key, v in res.items()}
+    print(json.dumps({"k": k, "m": m, "B": B, "GB": round(gb, 2), "verify_ok": [ok, ok_perm],
+                      "compiled": enc.compiled_network(), "ms": res,
+                      "TBps_best": {key: round(gb / v, 3) for key, v in best.items()}}), flush=True)
+    del stripes
+    torch.cuda.empty_cache()
