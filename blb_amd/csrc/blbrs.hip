@@ -1780,6 +1780,7 @@ int blbrs_pack_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_str
         a.rows = static_cast<uint32_t>(plan->passes[0].rows);
         a.table = tdev;
         a.nextents = nextents;
+        a.parity = plan->passes[0].parity;
         if (pack_encode_supported(a)) {
             const hipError_t e = launch_pack_encode(a, s);
             if (e != hipSuccess) return hip_fail(e, "launch pack_encode_kernel");

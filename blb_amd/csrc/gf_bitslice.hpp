@@ -123,6 +123,28 @@ constexpr Terms<K> make_terms() {
 template <int K>
 constexpr Terms<K> kTerms = make_terms<K>();
 
+// The same network grouped by input: for parity row j, output bit p and input c, the bits q
+// of input c to fold (kernels that consume one input at a time, e.g. PackTracts + Encode).
+template <int K>
+struct InputTerms {
+    int n[kMaxParity][8][K] = {};
+    uint8_t q[kMaxParity][8][K][8] = {};
+};
+template <int K>
+constexpr InputTerms<K> make_input_terms() {
+    InputTerms<K> t{};
+    for (int j = 0; j < kMaxParity; ++j)
+        for (int c = 0; c < K; ++c)
+            for (int q = 0; q < 8; ++q) {
+                const uint8_t col = cmul(kParity<K>.c[j][c], static_cast<uint8_t>(1u << q));
+                for (int p = 0; p < 8; ++p)
+                    if ((col >> p) & 1u) t.q[j][p][c][t.n[j][p][c]++] = static_cast<uint8_t>(q);
+            }
+    return t;
+}
+template <int K>
+constexpr InputTerms<K> kInputTerms = make_input_terms<K>();
+
 // Host side: true when `rows` (nrows x k, row-major) are parity rows 0..nrows-1 of k, i.e.
 // a pass the compiled network computes.
 template <int K>
@@ -186,6 +208,33 @@ __device__ __forceinline__ uint32_t fold(const uint32_t (&x)[K][8]) {
     } else {
         return dev::xor3(x[kTerms<K>.c[R][P][J]][kTerms<K>.q[R][P][J]],
                          x[kTerms<K>.c[R][P][J + 1]][kTerms<K>.q[R][P][J + 1]], fold<K, R, P, J + 2>(x));
+    }
+}
+
+// acc ^ the terms [J, n) of input C for parity row R, output bit P (x = input C's planes).
+template <int K, int R, int P, int C, int J>
+__device__ __forceinline__ uint32_t fold_input(const uint32_t (&x)[8], uint32_t acc) {
+    constexpr int n = kInputTerms<K>.n[R][P][C];
+    if constexpr (J >= n) {
+        return acc;
+    } else if constexpr (J + 1 == n) {
+        return acc ^ x[kInputTerms<K>.q[R][P][C][J]];
+    } else {
+        return fold_input<K, R, P, C, J + 2>(
+            x, dev::xor3(acc, x[kInputTerms<K>.q[R][P][C][J]], x[kInputTerms<K>.q[R][P][C][J + 1]]));
+    }
+}
+
+// Input C's contribution to the planes of parity rows R.. < MR (acc in plane form).
+template <int K, int MR, int C, int R = 0, int P = 0>
+__device__ __forceinline__ void add_input(const uint32_t (&x)[8], uint32_t (&acc)[MR][8]) {
+    if constexpr (R < MR) {
+        if constexpr (P < 8) {
+            acc[R][P] = fold_input<K, R, P, C, 0>(x, acc[R][P]);
+            add_input<K, MR, C, R, P + 1>(x, acc);
+        } else {
+            add_input<K, MR, C, R + 1, 0>(x, acc);
+        }
     }
 }
 

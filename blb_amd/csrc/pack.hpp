@@ -35,6 +35,7 @@ struct PackEncodeArgs {
     uint32_t B, k, rows;
     const uint64_t* table;    // device extent table (pieces = B * k)
     uint64_t nextents;        // extents in the table
+    bool parity = false;      // tables are encode parity rows 0..rows-1 of k (gf_bitslice.hpp)
 };
 // True when a fused instantiation covers the shape (k in blb's list, rows <= 5, 16-byte
 // aligned base and strides); otherwise the caller packs, then encodes.

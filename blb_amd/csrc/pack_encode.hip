@@ -23,6 +23,9 @@
 // bytes (pack.hip's rule), so no read touches a page the source does not own.
 #include "pack.hpp"
 
+#include <type_traits>
+
+#include "gf_bitslice.hpp"
 #include "gf_device.hpp"
 
 
@@ -174,8 +177,20 @@ __device__ V4 mixed_chunk(const uint64_t* ex, uint64_t e, uint64_t hi, uint64_t 
 // One workgroup per (stripe, tile); wave w owns the tile's bytes [w*U KiB, (w+1)*U KiB) of
 // every piece, chunk u of lane l at w*U KiB + u KiB + 16 l, so the 16-byte block after lane
 // 63's chunk u is lane 0's chunk u + 1 (a DPP rotate away) except after the last chunk.
-template <int K, int MR, int U>
+// f(integral_constant<int, I>) for I = 0..N-1 (compile-time piece indices for the network).
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+
+// CM: the parity rows are encode parity rows 0..MR-1 of K, accumulated in bit-plane form by
+// the compiled network (gf_bitslice.hpp) one piece at a time (U = 2: 8 dwords per lane).
+template <int K, int MR, int U, bool CM>
 __global__ __launch_bounds__(kPEThreads) void pack_encode_kernel(PEArgs a) {
+    static_assert(!CM || U == 2, "bit planes of 8 dwords");
     constexpr uint32_t kWaveRow = 64u * 16u;             // 1 KiB per wave instruction
     constexpr uint32_t kWaveRun = kWaveRow * U;          // contiguous bytes per wave
     constexpr uint32_t kTile = kWaveRun * (kPEThreads / 64u);
@@ -231,8 +246,8 @@ __global__ __launch_bounds__(kPEThreads) void pack_encode_kernel(PEArgs a) {
     uint32_t acc[MR][NV] = {};
     cu32 tables = as_const(a.tables);
     asm volatile("" : "+s"(tables));
-#pragma unroll
-    for (int p = 0; p < K; ++p) {
+    static_for<K>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
         V4 x[U];
         const uint32_t kd = kind(p);
         if (kd == kZero) {
@@ -273,8 +288,17 @@ __global__ __launch_bounds__(kPEThreads) void pack_encode_kernel(PEArgs a) {
         uint32_t xv[NV];
 #pragma unroll
         for (int u = 0; u < U; ++u) unpack(x[u], xv + 4 * u);
-        madd<MR, NV>(Groups<NV>(xv), [&](int r) { return tables + (r * K + p) * 5; }, acc, static_cast<int>(a.rows));
-    }
+        if constexpr (CM) {
+            bs::transpose8(xv);
+            bs::add_input<K, MR, p>(xv, acc);
+        } else {
+            madd<MR, NV>(Groups<NV>(xv), [&](int r) { return tables + (r * K + p) * 5; }, acc,
+                         static_cast<int>(a.rows));
+        }
+    });
+    if constexpr (CM)
+#pragma unroll
+        for (int r = 0; r < MR; ++r) bs::transpose8(acc[r]);
     const ci32 out_idx = as_const(a.out_idx);
 #pragma unroll
     for (int r = 0; r < MR; ++r) {
@@ -302,29 +326,43 @@ using KernelFn = void (*)(PEArgs);
 #endif
 constexpr int pe_u(uint32_t k) { return k <= 6 ? BLBRS_PE_U_NARROW : BLBRS_PE_U_WIDE; }
 
+// The network runs at U = 2 for every k: it holds fewer registers than the table multiply
+// (RS(12,5) 141 at U = 1 with tables).  BLBRS_PE_CM_WIDE=0 (A/B) keeps wide k on the U = 1
+// table kernel.
+bool cm_wide() {
+    const char* e = getenv("BLBRS_PE_CM_WIDE");
+    return !(e && e[0] == '0');
+}
+int tile_u(uint32_t k, bool cm) { return cm && (k <= 6 || cm_wide()) ? 2 : pe_u(k); }
+
+template <int K, int MR>
+KernelFn pick_cm(bool cm) {
+    if (cm && tile_u(K, cm) == 2) return pack_encode_kernel<K, MR, 2, true>;
+    return pack_encode_kernel<K, MR, pe_u(K), false>;
+}
+
 template <int K>
-KernelFn pick_rows(uint32_t rows) {
-    constexpr int U = pe_u(K);
+KernelFn pick_rows(uint32_t rows, bool cm) {
     switch (rows) {
-        case 1: return pack_encode_kernel<K, 1, U>;
-        case 2: return pack_encode_kernel<K, 2, U>;
-        case 3: return pack_encode_kernel<K, 3, U>;
-        case 4: return pack_encode_kernel<K, 4, U>;
-        case 5: return pack_encode_kernel<K, 5, U>;
+        case 1: return pick_cm<K, 1>(cm);
+        case 2: return pick_cm<K, 2>(cm);
+        case 3: return pick_cm<K, 3>(cm);
+        case 4: return pick_cm<K, 4>(cm);
+        case 5: return pick_cm<K, 5>(cm);
         default: return nullptr;
     }
 }
 
 // blb's classes RS(6,3), RS(8,3), RS(10,3), RS(12,5), the bench's RS(10,4), the reference
-// tests' RS(3,2) and RS(4,2).
-KernelFn pick(uint32_t k, uint32_t rows) {
+// tests' RS(3,2) and RS(4,2).  cm: the compiled encode network (parity-row tables).
+KernelFn pick(uint32_t k, uint32_t rows, bool cm = false) {
     switch (k) {
-        case 3: return pick_rows<3>(rows);
-        case 4: return pick_rows<4>(rows);
-        case 6: return pick_rows<6>(rows);
-        case 8: return pick_rows<8>(rows);
-        case 10: return pick_rows<10>(rows);
-        case 12: return pick_rows<12>(rows);
+        case 3: return pick_rows<3>(rows, cm);
+        case 4: return pick_rows<4>(rows, cm);
+        case 6: return pick_rows<6>(rows, cm);
+        case 8: return pick_rows<8>(rows, cm);
+        case 10: return pick_rows<10>(rows, cm);
+        case 12: return pick_rows<12>(rows, cm);
         default: return nullptr;
     }
 }
@@ -334,7 +372,7 @@ KernelFn pick(uint32_t k, uint32_t rows) {
 bool pack_encode_supported(const PackEncodeArgs& a) {
     const bool aligned = (reinterpret_cast<uintptr_t>(a.base) & 15u) == 0 && (a.shard_stride & 15u) == 0 &&
                          (a.stripe_stride & 15u) == 0;
-    const uint64_t tile = 4096ull * pe_u(a.k);
+    const uint64_t tile = 4096ull * tile_u(a.k, a.parity && bs::enabled());
     return a.base && aligned && pick(a.k, a.rows) != nullptr && a.nextents <= 0xFFFFFFFFull &&
            static_cast<uint64_t>(a.B) * ((a.S + tile - 1) / tile) <= 0x7FFFFFFFull;
 }
@@ -342,7 +380,8 @@ bool pack_encode_supported(const PackEncodeArgs& a) {
 hipError_t launch_pack_encode(const PackEncodeArgs& in, hipStream_t stream) {
     if (in.B == 0 || in.S == 0) return hipSuccess;
     if (!pack_encode_supported(in)) return hipErrorInvalidValue;
-    const uint64_t tile = 4096ull * pe_u(in.k);
+    const bool cm = in.parity && bs::enabled();
+    const uint64_t tile = 4096ull * tile_u(in.k, cm);
     const uint64_t ndesc = static_cast<uint64_t>(in.B) * in.k * ((in.S + tile - 1) / tile);
     if (ndesc > 0xFFFFFFFFull * 256) return hipErrorInvalidValue;
     PEArgs a{};
@@ -369,7 +408,8 @@ hipError_t launch_pack_encode(const PackEncodeArgs& in, hipStream_t stream) {
                        in.k, desc);
     e = hipGetLastError();
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(pick(in.k, in.rows), dim3(static_cast<unsigned>(grid)), dim3(kPEThreads), 0, stream, a);
+        hipLaunchKernelGGL(pick(in.k, in.rows, cm), dim3(static_cast<unsigned>(grid)),
+                           dim3(kPEThreads), 0, stream, a);
         e = hipGetLastError();
     }
     const hipError_t f = hipFreeAsync(desc, stream);

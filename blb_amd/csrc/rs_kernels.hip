@@ -300,6 +300,16 @@ constexpr int pick_u(int K, int MR, int MODE) {
     return MODE == 0 ? ((K > 0 && K + MR <= 9) ? 4 : BLBRS_U_WIDE) : (K + MR > 13 ? BLBRS_U_VERIFY_WIDE : 2);  // MODE 1, 2
 }
 
+// The compiled network holds fewer registers than the table multiply (no bit groups, no
+// table operands): verify keeps U = 2 on every shape (RS(12,5): 154 VGPRs), and encode may
+// take BLBRS_CM_U_WIDE chunks on wide shapes (A/B builds; default as the table kernel).
+#ifndef BLBRS_CM_U_WIDE
+#define BLBRS_CM_U_WIDE BLBRS_U_WIDE
+#endif
+constexpr int pick_u_cm(int K, int MR, int MODE) {
+    return MODE == 0 ? (K + MR <= 9 ? 4 : BLBRS_CM_U_WIDE) : 2;
+}
+
 template <int K, int MR, int MODE, int ADDR>
 constexpr KernelFn fn_of() { return rs_code_kernel<K, MR, MODE, ADDR, pick_u(K, MR, MODE), kNT>; }
 
@@ -313,11 +323,11 @@ struct Choice {
 // Encode / Verify passes of parity rows: the compiled network where the shape has one.
 template <int K, int MR, int MODE, int ADDR>
 Choice choice_of(bool cm) {
-    constexpr int U = pick_u(K, MR, MODE);
-    if constexpr (K > 0 && U % 2 == 0 && MODE != 2) {
-        if (cm) return {rs_code_kernel<K, MR, MODE, ADDR, U, kNT, true>, U, true, true};
+    constexpr int UC = pick_u_cm(K, MR, MODE);
+    if constexpr (K > 0 && UC % 2 == 0 && MODE != 2) {
+        if (cm) return {rs_code_kernel<K, MR, MODE, ADDR, UC, kNT, true>, UC, true, true};
     }
-    return {fn_of<K, MR, MODE, ADDR>(), U, K > 0, false};
+    return {fn_of<K, MR, MODE, ADDR>(), pick_u(K, MR, MODE), K > 0, false};
 }
 
 template <int K, int MODE, int ADDR>

@@ -7,9 +7,11 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from blb_amd import pack  # noqa: E402
 from blb_amd import reedsolomon as rs  # noqa: E402
 
 p = argparse.ArgumentParser()
@@ -40,7 +42,33 @@ for spec in a.shapes.split(";"):
     k, m, B = (int(v) for v in spec.split(","))
     stripes = torch.randint(0, 256, (B, k + m, S), dtype=torch.uint8, device=dev)
     enc = rs.New(k, m)
-    ops = {"encode": lambda: enc.EncodeBatch(stripes),
+    ext = []
+    if "pack_encode" in a.ops:
+        # tracts of 64 KiB..8 MiB from a 4 GiB pool at padToLength-aligned piece offsets (bench.py)
+        pool = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev)
+        prng = np.random.default_rng(17)
+        for piece in range(B * k):
+            off = 0
+            while True:
+                ln = int(prng.integers(64 << 10, (8 << 20) + 1))
+                if off + ln > S:
+                    break
+                ext.append((pool[int(prng.integers(0, pool.numel() - ln)):], off, ln, piece))
+                off += pack.padded_length(ln)
+
+    def pack_encode_ms():
+        pack.PackEncode(enc, stripes, ext)
+        torch.cuda.synchronize(dev)
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(400_000_000)  # host-side extent checks outside the window
+        s0.record()
+        pack.PackEncode(enc, stripes, ext)
+        s1.record()
+        torch.cuda.synchronize(dev)
+        return s0.elapsed_time(s1)
+
+    ops = {"pack_encode": pack_encode_ms,
+           "encode": lambda: enc.EncodeBatch(stripes),
            "verify": lambda: enc.VerifyBatch(stripes),
            "encode_crc": lambda: enc.EncodeBatchCRC(stripes, 65532)}
     variants = []
@@ -52,7 +80,8 @@ for spec in a.shapes.split(";"):
         for vname, env in variants:
             os.environ.update(env)
             for name in a.ops.split(","):
-                res.setdefault(f"{name}_{vname}", []).append(round(timed(ops[name]), 3))
+                ms = ops[name]() if name == "pack_encode" else timed(ops[name])
+                res.setdefault(f"{name}_{vname}", []).append(round(ms, 3))
             for key in env:
                 os.environ.pop(key, None)
     # the two paths write the same parity
@@ -66,5 +95,6 @@ for spec in a.shapes.split(";"):
     print(json.dumps({"k": k, "m": m, "B": B, "GB": round(gb, 2), "verify_ok": [ok, ok_perm],
                       "compiled": enc.compiled_network(), "ms": res,
                       "TBps_best": {key: round(gb / v, 3) for key, v in best.items()}}), flush=True)
-    del stripes
+    del stripes, ext
+    pool = None
     torch.cuda.empty_cache()
