@@ -1060,10 +1060,10 @@ int blbrs_data_shards(const blbrs_encoder* enc) { return enc ? enc->k : 0; }
 int blbrs_parity_shards(const blbrs_encoder* enc) { return enc ? enc->m : 0; }
 
 int blbrs_encoder_compiled_network(const blbrs_encoder* enc) {
-    if (!enc || !bs::enabled()) return 0;
+    if (!enc) return 0;
     const auto hp = enc->core->encode_plan();
     for (const Pass& ps : hp->passes)
-        if (!ps.parity) return 0;
+        if (!bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode)) return 0;
     return 1;
 }
 

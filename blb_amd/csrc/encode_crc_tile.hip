@@ -363,15 +363,6 @@ __device__ __forceinline__ void load_tile(const TArgs& a, const uint8_t* stripe,
     }
 }
 
-// Parity rows R.. of the compiled encode network (gf_bitslice.hpp) from the input planes.
-template <int K, int MR, int R>
-__device__ __forceinline__ void bs_rows(const uint32_t (&x)[K][8], uint32_t (&acc)[MR][8]) {
-    if constexpr (R < MR) {
-        bs::parity_row<K, R>(x, acc[R]);
-        bs_rows<K, MR, R + 1>(x, acc);
-    }
-}
-
 // The parity rows of the tile, stored nontemporal; acc keeps them.  CM: the plan's rows are
 // encode parity rows 0..MR-1 of K, computed by the compiled bit-plane XOR network (the
 // inputs are transposed in place); otherwise the v_perm multiply with the plan's tables.
@@ -383,9 +374,13 @@ __device__ __forceinline__ void code_tile(const TArgs& a, uint8_t* stripe, uint6
     const ci32 out_idx = as_const(a.out_idx);
     if constexpr (CM) {
         static_assert(NV == 8, "bit planes of 8 dwords");
+#ifdef BLBRS_ECT_CM_PAIRS  // A/B: fold input pairs as their loads land
+        bs::parity_rows_by_pairs<K, MR>(x, acc);
+#else
 #pragma unroll
         for (int c = 0; c < K; ++c) bs::transpose8(x[c]);
-        bs_rows<K, MR, 0>(x, acc);
+        bs::parity_rows<K, MR>(x, acc);
+#endif
     } else {
         cu32 tables = as_const(a.tables);
         asm volatile("" : "+s"(tables));
@@ -765,7 +760,7 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     if (in.B == 0 || in.S == 0) return hipSuccess;
     if (!encode_crc_tile_supported(in) || !in.crc) return hipErrorInvalidValue;
     const int lc = lc_for(in.k, in.rows);
-    const bool cm = in.parity && bs::enabled();
+    const bool cm = bs::use(in.parity, in.k, in.rows, bs::kWideTile);
     const KernelFn fn = pick(in.k, in.rows, false, cm);
     const CrcConsts* c = nullptr;
     hipError_t e = crc_consts_for(65536, &c);  // tables + pow2 (the segment size is irrelevant here)

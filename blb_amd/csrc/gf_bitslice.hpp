@@ -123,27 +123,35 @@ constexpr Terms<K> make_terms() {
 template <int K>
 constexpr Terms<K> kTerms = make_terms<K>();
 
-// The same network grouped by input: for parity row j, output bit p and input c, the bits q
-// of input c to fold (kernels that consume one input at a time, e.g. PackTracts + Encode).
-template <int K>
-struct InputTerms {
-    int n[kMaxParity][8][K] = {};
-    uint8_t q[kMaxParity][8][K][8] = {};
+// The same network grouped by inputs: for parity row j, output bit p and input group g
+// (inputs [G*g, G*g + G)), the planes (c, q) to fold.  Kernels that fold inputs as their loads
+// arrive (G = 2: the coding kernels, one pair at a time) or one at a time (G = 1: PackTracts
+// + Encode, which assembles pieces sequentially).
+template <int K, int G>
+struct GroupTerms {
+    static constexpr int kGroups = (K + G - 1) / G;
+    int n[kMaxParity][8][kGroups] = {};
+    uint8_t c[kMaxParity][8][kGroups][8 * G] = {};
+    uint8_t q[kMaxParity][8][kGroups][8 * G] = {};
 };
-template <int K>
-constexpr InputTerms<K> make_input_terms() {
-    InputTerms<K> t{};
+template <int K, int G>
+constexpr GroupTerms<K, G> make_group_terms() {
+    GroupTerms<K, G> t{};
     for (int j = 0; j < kMaxParity; ++j)
         for (int c = 0; c < K; ++c)
             for (int q = 0; q < 8; ++q) {
                 const uint8_t col = cmul(kParity<K>.c[j][c], static_cast<uint8_t>(1u << q));
                 for (int p = 0; p < 8; ++p)
-                    if ((col >> p) & 1u) t.q[j][p][c][t.n[j][p][c]++] = static_cast<uint8_t>(q);
+                    if ((col >> p) & 1u) {
+                        const int g = c / G, i = t.n[j][p][g]++;
+                        t.c[j][p][g][i] = static_cast<uint8_t>(c);
+                        t.q[j][p][g][i] = static_cast<uint8_t>(q);
+                    }
             }
     return t;
 }
-template <int K>
-constexpr InputTerms<K> kInputTerms = make_input_terms<K>();
+template <int K, int G>
+constexpr GroupTerms<K, G> kGroupTerms = make_group_terms<K, G>();
 
 // Host side: true when `rows` (nrows x k, row-major) are parity rows 0..nrows-1 of k, i.e.
 // a pass the compiled network computes.
@@ -167,11 +175,23 @@ inline bool is_parity_rows(const uint8_t* rows, int nrows, int k) {
     }
 }
 
-// BLBRS_BITSLICE=0, read per launch, runs encode passes on the v_perm path (A/B runs).
-inline bool enabled() {
+// Which encode passes take the network (tools/bitslice_ab.py): the shapes where
+// the table multiply is VALU-bound, k + rows > `wide` (each kernel passes its own measured
+// threshold).  Where the table kernel already runs at the access pattern's speed (RS(6,3)) it
+// folds each input pair as its loads land and stays 2-5 % ahead of the network.
+// BLBRS_BITSLICE, read per launch (A/B runs): 0 = never, 2 = every compiled shape.
+inline int mode() {
     const char* e = getenv("BLBRS_BITSLICE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
 }
+inline bool use(bool parity, int k, int rows, int wide) {
+    if (!parity) return false;
+    const int m = mode();
+    return m == 2 || (m == 1 && k + rows > wide);
+}
+// Thresholds per kernel: rs_code_kernel (k + rows > 9 is also where it drops to U = 2), the
+// fused encode+CRC tile kernel, PackTracts + Encode.
+constexpr int kWideCode = 9, kWideTile = 11, kWidePack = 9;
 
 // --- device ----------------------------------------------------------------------------
 
@@ -202,39 +222,16 @@ __device__ __forceinline__ uint32_t fold(const uint32_t (&x)[K][8]) {
     if constexpr (J >= n) {
         return 0u;
     } else if constexpr (J + 1 == n) {
-        return x[kTerms<K>.c[R][P][J]][kTerms<K>.q[R][P][J]];
+        constexpr int c0 = kTerms<K>.c[R][P][J], q0 = kTerms<K>.q[R][P][J];
+        return x[c0][q0];
     } else if constexpr (J + 2 == n) {
-        return x[kTerms<K>.c[R][P][J]][kTerms<K>.q[R][P][J]] ^ x[kTerms<K>.c[R][P][J + 1]][kTerms<K>.q[R][P][J + 1]];
+        constexpr int c0 = kTerms<K>.c[R][P][J], q0 = kTerms<K>.q[R][P][J];
+        constexpr int c1 = kTerms<K>.c[R][P][J + 1], q1 = kTerms<K>.q[R][P][J + 1];
+        return x[c0][q0] ^ x[c1][q1];
     } else {
-        return dev::xor3(x[kTerms<K>.c[R][P][J]][kTerms<K>.q[R][P][J]],
-                         x[kTerms<K>.c[R][P][J + 1]][kTerms<K>.q[R][P][J + 1]], fold<K, R, P, J + 2>(x));
-    }
-}
-
-// acc ^ the terms [J, n) of input C for parity row R, output bit P (x = input C's planes).
-template <int K, int R, int P, int C, int J>
-__device__ __forceinline__ uint32_t fold_input(const uint32_t (&x)[8], uint32_t acc) {
-    constexpr int n = kInputTerms<K>.n[R][P][C];
-    if constexpr (J >= n) {
-        return acc;
-    } else if constexpr (J + 1 == n) {
-        return acc ^ x[kInputTerms<K>.q[R][P][C][J]];
-    } else {
-        return fold_input<K, R, P, C, J + 2>(
-            x, dev::xor3(acc, x[kInputTerms<K>.q[R][P][C][J]], x[kInputTerms<K>.q[R][P][C][J + 1]]));
-    }
-}
-
-// Input C's contribution to the planes of parity rows R.. < MR (acc in plane form).
-template <int K, int MR, int C, int R = 0, int P = 0>
-__device__ __forceinline__ void add_input(const uint32_t (&x)[8], uint32_t (&acc)[MR][8]) {
-    if constexpr (R < MR) {
-        if constexpr (P < 8) {
-            acc[R][P] = fold_input<K, R, P, C, 0>(x, acc[R][P]);
-            add_input<K, MR, C, R, P + 1>(x, acc);
-        } else {
-            add_input<K, MR, C, R + 1, 0>(x, acc);
-        }
+        constexpr int c0 = kTerms<K>.c[R][P][J], q0 = kTerms<K>.q[R][P][J];
+        constexpr int c1 = kTerms<K>.c[R][P][J + 1], q1 = kTerms<K>.q[R][P][J + 1];
+        return dev::xor3(x[c0][q0], x[c1][q1], fold<K, R, P, J + 2>(x));
     }
 }
 
@@ -246,13 +243,95 @@ __device__ __forceinline__ void row_planes(const uint32_t (&x)[K][8], uint32_t* 
     }
 }
 
-// Parity row R of 8 dwords per input: x holds the K inputs' planes (transposed in place by
-// the caller), out gets the row's 8 dwords in byte form.
-template <int K, int R>
-__device__ __forceinline__ void parity_row(const uint32_t (&x)[K][8], uint32_t* out) {
-    static_assert(R < kMaxParity, "parity row");
-    row_planes<K, R, 0>(x, out);
-    transpose8(out);
+// Parity rows 0..MR-1 (x transposed in place by the caller), rows in byte form.
+template <int K, int MR, int R = 0>
+__device__ __forceinline__ void parity_rows(const uint32_t (&x)[K][8], uint32_t (&out)[MR][8]) {
+    if constexpr (R < MR) {
+        row_planes<K, R, 0>(x, out[R]);
+        transpose8(out[R]);
+        parity_rows<K, MR, R + 1>(x, out);
+    }
+}
+
+// acc ^ the terms [J, n) of input group GI for parity row R, output bit P (x: every input's
+// planes, those of group GI transposed).  Every index is bound to a constexpr int first:
+// used directly as a subscript, a member of the constexpr table may be read from memory at
+// run time, and x then lives in scratch.
+template <int K, int G, int R, int P, int GI, int J>
+__device__ __forceinline__ uint32_t fold_group(const uint32_t (&x)[K][8], uint32_t acc) {
+    constexpr int n = kGroupTerms<K, G>.n[R][P][GI];
+    if constexpr (J >= n) {
+        return acc;
+    } else if constexpr (J + 1 == n) {
+        constexpr int c0 = kGroupTerms<K, G>.c[R][P][GI][J], q0 = kGroupTerms<K, G>.q[R][P][GI][J];
+        return acc ^ x[c0][q0];
+    } else {
+        constexpr int c0 = kGroupTerms<K, G>.c[R][P][GI][J], q0 = kGroupTerms<K, G>.q[R][P][GI][J];
+        constexpr int c1 = kGroupTerms<K, G>.c[R][P][GI][J + 1], q1 = kGroupTerms<K, G>.q[R][P][GI][J + 1];
+        return fold_group<K, G, R, P, GI, J + 2>(x, dev::xor3(acc, x[c0][q0], x[c1][q1]));
+    }
+}
+
+// Input group GI's contribution to the planes of parity rows R.. < MR (acc in plane form).
+template <int K, int G, int MR, int GI, int R = 0, int P = 0>
+__device__ __forceinline__ void add_group(const uint32_t (&x)[K][8], uint32_t (&acc)[MR][8]) {
+    if constexpr (R < MR) {
+        if constexpr (P < 8) {
+            acc[R][P] = fold_group<K, G, R, P, GI, 0>(x, acc[R][P]);
+            add_group<K, G, MR, GI, R, P + 1>(x, acc);
+        } else {
+            add_group<K, G, MR, GI, R + 1, 0>(x, acc);
+        }
+    }
+}
+
+// One input C at a time (G = 1 terms; x = input C's planes only).
+template <int K, int R, int P, int C, int J>
+__device__ __forceinline__ uint32_t fold_one(const uint32_t (&x)[8], uint32_t acc) {
+    constexpr int n = kGroupTerms<K, 1>.n[R][P][C];
+    if constexpr (J >= n) {
+        return acc;
+    } else if constexpr (J + 1 == n) {
+        constexpr int q0 = kGroupTerms<K, 1>.q[R][P][C][J];
+        return acc ^ x[q0];
+    } else {
+        constexpr int q0 = kGroupTerms<K, 1>.q[R][P][C][J], q1 = kGroupTerms<K, 1>.q[R][P][C][J + 1];
+        return fold_one<K, R, P, C, J + 2>(x, dev::xor3(acc, x[q0], x[q1]));
+    }
+}
+template <int K, int MR, int C, int R = 0, int P = 0>
+__device__ __forceinline__ void add_one(const uint32_t (&x)[8], uint32_t (&acc)[MR][8]) {
+    if constexpr (R < MR) {
+        if constexpr (P < 8) {
+            acc[R][P] = fold_one<K, R, P, C, 0>(x, acc[R][P]);
+            add_one<K, MR, C, R, P + 1>(x, acc);
+        } else {
+            add_one<K, MR, C, R + 1, 0>(x, acc);
+        }
+    }
+}
+
+// Parity rows 0..MR-1 of 8 dwords per input, folding input pairs in order so that the work
+// on a pair can start as soon as its loads land: x holds the inputs in byte form and is
+// transposed in place pair by pair; acc gets the rows in byte form.
+template <int K, int MR, int GI = 0>
+__device__ __forceinline__ void parity_rows_by_pairs(uint32_t (&x)[K][8], uint32_t (&acc)[MR][8]) {
+    constexpr int kPairs = (K + 1) / 2;
+    if constexpr (GI == 0) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r)
+#pragma unroll
+            for (int d = 0; d < 8; ++d) acc[r][d] = 0u;
+    }
+    if constexpr (GI < kPairs) {
+        transpose8(x[2 * GI]);
+        if constexpr (2 * GI + 1 < K) transpose8(x[2 * GI + 1]);
+        add_group<K, 2, MR, GI>(x, acc);
+        parity_rows_by_pairs<K, MR, GI + 1>(x, acc);
+    } else {
+#pragma unroll
+        for (int r = 0; r < MR; ++r) transpose8(acc[r]);
+    }
 }
 
 }  // namespace bs

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(kPEThreads) void pack_encode_kernel(PEArgs a) {
         for (int u = 0; u < U; ++u) unpack(x[u], xv + 4 * u);
         if constexpr (CM) {
             bs::transpose8(xv);
-            bs::add_input<K, MR, p>(xv, acc);
+            bs::add_one<K, MR, p>(xv, acc);
         } else {
             madd<MR, NV>(Groups<NV>(xv), [&](int r) { return tables + (r * K + p) * 5; }, acc,
                          static_cast<int>(a.rows));
@@ -372,7 +372,7 @@ KernelFn pick(uint32_t k, uint32_t rows, bool cm = false) {
 bool pack_encode_supported(const PackEncodeArgs& a) {
     const bool aligned = (reinterpret_cast<uintptr_t>(a.base) & 15u) == 0 && (a.shard_stride & 15u) == 0 &&
                          (a.stripe_stride & 15u) == 0;
-    const uint64_t tile = 4096ull * tile_u(a.k, a.parity && bs::enabled());
+    const uint64_t tile = 4096ull * tile_u(a.k, bs::use(a.parity, static_cast<int>(a.k), static_cast<int>(a.rows), bs::kWidePack));
     return a.base && aligned && pick(a.k, a.rows) != nullptr && a.nextents <= 0xFFFFFFFFull &&
            static_cast<uint64_t>(a.B) * ((a.S + tile - 1) / tile) <= 0x7FFFFFFFull;
 }
@@ -380,7 +380,7 @@ bool pack_encode_supported(const PackEncodeArgs& a) {
 hipError_t launch_pack_encode(const PackEncodeArgs& in, hipStream_t stream) {
     if (in.B == 0 || in.S == 0) return hipSuccess;
     if (!pack_encode_supported(in)) return hipErrorInvalidValue;
-    const bool cm = in.parity && bs::enabled();
+    const bool cm = bs::use(in.parity, static_cast<int>(in.k), static_cast<int>(in.rows), bs::kWidePack);
     const uint64_t tile = 4096ull * tile_u(in.k, cm);
     const uint64_t ndesc = static_cast<uint64_t>(in.B) * in.k * ((in.S + tile - 1) / tile);
     if (ndesc > 0xFFFFFFFFull * 256) return hipErrorInvalidValue;

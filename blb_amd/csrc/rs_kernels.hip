@@ -35,6 +35,17 @@
 #include "gf_bitslice.hpp"
 #include "gf_device.hpp"
 
+// Network path A/B knobs (tools/ect_variants.sh builds):
+//  BLBRS_CM_PAIRS 1 = the network folds input pairs as their loads land (longer live ranges); 0 = one fold per 8-dword group after its loads.
+#ifndef BLBRS_CM_PAIRS
+#define BLBRS_CM_PAIRS 0
+#endif
+// 1 = group-major loads and per-group stores in the network path; 0 = input-major loads and
+// every store after the math, as the table path.
+#ifndef BLBRS_CM_GROUP_LOADS
+#define BLBRS_CM_GROUP_LOADS 1
+#endif
+
 namespace blbrs {
 namespace {
 
@@ -125,15 +136,6 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
     }
 }
 
-// Parity rows R.. of the compiled encode network over one 8-dword group of every input.
-template <int K, int MR, int R>
-__device__ __forceinline__ void bs_rows(const uint32_t (&xs)[K][8], uint32_t (&acc)[MR][8]) {
-    if constexpr (R < MR) {
-        bs::parity_row<K, R>(xs, acc[R]);
-        bs_rows<K, MR, R + 1>(xs, acc);
-    }
-}
-
 // K > 0: compile-time input count (all K*U chunk loads issued before any math).
 // K == 0: runtime k (loads issued per input, two inputs unrolled).
 // MR: compile-time bound on output rows; a.rows <= MR honoured at runtime.
@@ -190,13 +192,27 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
 
         if constexpr (K > 0) {
             V4 x[K][U];
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
-#pragma unroll
-                for (int u = 0; u < U; ++u) x[c][u] = ld16<NT>(p + u * kStep);
-            }
             if constexpr (CM) {
+                // Group-major loads (chunks 2g, 2g+1 of every input, g = 0 first), so that group
+                // 0's network starts while group 1 is still in flight; within a group the
+                // network folds input pairs as they land.
+#if BLBRS_CM_GROUP_LOADS
+#pragma unroll
+                for (int g = 0; g < U / 2; ++g)
+#pragma unroll
+                    for (int c = 0; c < K; ++c) {
+                        const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
+                        x[c][2 * g] = ld16<NT>(p + 2 * g * kStep);
+                        x[c][2 * g + 1] = ld16<NT>(p + (2 * g + 1) * kStep);
+                    }
+#else
+#pragma unroll
+                for (int c = 0; c < K; ++c) {
+                    const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) x[c][u] = ld16<NT>(p + u * kStep);
+                }
+#endif
 #pragma unroll
                 for (int g = 0; g < U / 2; ++g) {
                     uint32_t xs[K][8], og[MR][8];
@@ -204,15 +220,34 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
                     for (int c = 0; c < K; ++c) {
                         unpack(x[c][2 * g], xs[c]);
                         unpack(x[c][2 * g + 1], xs[c] + 4);
-                        bs::transpose8(xs[c]);
                     }
-                    bs_rows<K, MR, 0>(xs, og);
+#if BLBRS_CM_PAIRS
+                    bs::parity_rows_by_pairs<K, MR>(xs, og);
+#else
+#pragma unroll
+                    for (int c = 0; c < K; ++c) bs::transpose8(xs[c]);
+                    bs::parity_rows<K, MR>(xs, og);
+#endif
 #pragma unroll
                     for (int r = 0; r < MR; ++r)
 #pragma unroll
                         for (int d = 0; d < 8; ++d) acc[r][8 * g + d] = og[r][d];
+                    if constexpr (MODE == 0 && BLBRS_CM_GROUP_LOADS) {  // this group's stores go out before the next group's math
+#pragma unroll
+                        for (int r = 0; r < MR; ++r) {
+                            uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
+                            st16<NT>(q + 2 * g * kStep, pack(acc[r] + 8 * g));
+                            st16<NT>(q + (2 * g + 1) * kStep, pack(acc[r] + 8 * g + 4));
+                        }
+                    }
                 }
             } else {
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const uint8_t* p = shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off;
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[c][u] = ld16<NT>(p + u * kStep);
+            }
 #pragma unroll
             for (int c = 0; c + 1 < K; c += 2) {
                 uint32_t xa[NV], xb[NV];
@@ -259,7 +294,9 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
         for (int r = 0; r < MR; ++r) {
             if (r >= nr) break;
             uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
-            if (MODE == 0 || (MODE == 2 && r < a.nstore)) {
+            if (CM && MODE == 0 && BLBRS_CM_GROUP_LOADS) {
+                // stored per group above
+            } else if (MODE == 0 || (MODE == 2 && r < a.nstore)) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) st16<NT>(q + u * kStep, pack(acc[r] + 4 * u));
             } else {
@@ -380,7 +417,7 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream) {
     if (mode != Mode::kStore && !args.mismatch) return hipErrorInvalidValue;
     if (mode == Mode::kStoreVerify && (args.nstore < 0 || args.nstore > args.rows)) return hipErrorInvalidValue;
     if (args.B == 0 || args.S == 0) return hipSuccess;
-    const Choice ch = pick(args.k, args.rows, mode, args.base != nullptr, args.parity && bs::enabled());
+    const Choice ch = pick(args.k, args.rows, mode, args.base != nullptr, bs::use(args.parity, args.k, args.rows, bs::kWideCode));
     if (!ch.fn) return hipErrorInvalidValue;
     const uint64_t tile = static_cast<uint64_t>(kTileBytes) * ch.u;
     const uint64_t tps = (args.S + tile - 1) / tile;
@@ -408,7 +445,7 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream) {
 }
 
 const char* kernel_name(int k, int rows, Mode mode, bool parity) {
-    const Choice ch = pick(k, rows, mode, true, parity && bs::enabled());
+    const Choice ch = pick(k, rows, mode, true, bs::use(parity, k, rows, bs::kWideCode));
     return ch.cm      ? "rs_code_kernel<K,MR,MODE,ADDR,U,NT,true>"
            : ch.fixed ? "rs_code_kernel<K,MR,MODE,ADDR,U,NT>"
                       : "rs_code_kernel<0,MR,MODE,ADDR,U,NT>";

@@ -129,8 +129,9 @@ int blbrs_parity_shards(const blbrs_encoder* enc);
 int blbrs_matrix(const blbrs_encoder* enc, uint8_t* out, size_t cap);
 /* 1 when this encoder's Encode / Verify passes run the compiled bit-plane network (the
  * parity rows of (k, m) built into the library, gf_bitslice.hpp: k in {3,4,6,8,10,12},
- * m <= 5, and BLBRS_BITSLICE not "0"), 0 when they run the v_perm table path.  Same bytes
- * either way; a diagnostic for tests and profiles. */
+ * m <= 5; by default only where it is faster, k + m > 9; BLBRS_BITSLICE=0 never, =2 every
+ * compiled shape), 0 when they run the v_perm table path.  Same bytes either way; a
+ * diagnostic for tests and profiles. */
 int blbrs_encoder_compiled_network(const blbrs_encoder* enc);
 
 /* ---- host-memory Encoder methods (what the cgo shim binds) ---- */

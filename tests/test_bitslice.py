@@ -1,5 +1,6 @@
 """The compiled bit-plane encode network (gf_bitslice.hpp) against the oracle and against the
-v_perm table path it replaces for encode passes (BLBRS_BITSLICE=0, read per launch).
+v_perm table path it replaces for encode passes.  BLBRS_BITSLICE (read per launch) = 2 puts
+every compiled shape on the network (by default only k + m > 9), = 0 on the tables.
 
 Every compiled shape (k in {3, 4, 6, 8, 10, 12}, m = 1..5) runs through the four kernels that
 carry the network -- rs_code_kernel in store and verify mode, the fused encode+CRC tile kernel
@@ -34,6 +35,7 @@ def test_network_encode_verify_vs_oracle_and_tables(oracle_lib, k, m, monkeypatc
     rng = np.random.default_rng(1000 * k + m)
     host = rng.integers(0, 256, (B, k + m, S), dtype=np.uint8)
     host[:, k:] = 0xEE
+    monkeypatch.setenv("BLBRS_BITSLICE", "2")
     enc = rs.New(k, m)
     assert enc.compiled_network()
     st = torch.from_numpy(host).cuda()
@@ -68,13 +70,13 @@ def test_network_encode_crc_vs_oracle(oracle_lib, k, m, monkeypatch):
     host[:, k:] = 0xEE
     enc = rs.New(k, m)
     outs = {}
-    for mode in ("1", "0"):
+    for mode in ("2", "0"):
         monkeypatch.setenv("BLBRS_BITSLICE", mode)
         st = torch.from_numpy(host).cuda()
         crc = enc.EncodeBatchCRC(st, 65532).cpu().numpy().view(np.uint32)
         outs[mode] = (st.cpu().numpy(), crc)
-    assert np.array_equal(outs["1"][0], outs["0"][0]) and np.array_equal(outs["1"][1], outs["0"][1])
-    got, crc = outs["1"]
+    assert np.array_equal(outs["2"][0], outs["0"][0]) and np.array_equal(outs["2"][1], outs["0"][1])
+    got, crc = outs["2"]
     for b in range(B):
         want = _oracle_parity(oracle_lib, k, m, [host[b, i] for i in range(k)])
         for j in range(m):
@@ -102,11 +104,11 @@ def test_network_pack_encode_vs_tables(k, m, monkeypatch):
             off += ln + int(rng.integers(0, 3000))
     enc = rs.New(k, m)
     res = {}
-    for mode in ("1", "0"):
+    for mode in ("2", "0"):
         monkeypatch.setenv("BLBRS_BITSLICE", mode)
         st = torch.full((B, k + m, S), 0x5C, dtype=torch.uint8, device="cuda")
         pack.PackEncode(enc, st, ext)
         res[mode] = st
-    assert torch.equal(res["1"], res["0"])
+    assert torch.equal(res["2"], res["0"])
     monkeypatch.delenv("BLBRS_BITSLICE")
-    assert bool(enc.VerifyBatch(res["1"]).all())
+    assert bool(enc.VerifyBatch(res["2"]).all())

@@ -110,13 +110,19 @@ def test_c_abi_null_arguments():
 
 def test_compiled_network_covers_blb_classes(monkeypatch):
     """The parity rows built into the library (gf_bitslice.hpp, constexpr buildMatrix) equal
-    the runtime matrix for every compiled (k, m): Encode / Verify of those shapes run the
-    bit-plane network.  Other shapes, and BLBRS_BITSLICE=0, keep the v_perm table path."""
+    the runtime matrix for every compiled (k, m) -- with BLBRS_BITSLICE=2 Encode / Verify of
+    all 30 shapes run the bit-plane network.  By default only the wide shapes do (k + m > 9,
+    where the table multiply is VALU-bound); other shapes and BLBRS_BITSLICE=0 keep the
+    v_perm table path."""
     from blb_amd import reedsolomon as rs
+    monkeypatch.setenv("BLBRS_BITSLICE", "2")
     for k in (3, 4, 6, 8, 10, 12):
         for m in range(1, 6):
             assert rs.New(k, m).compiled_network(), (k, m)
     for k, m in ((5, 3), (10, 6), (2, 2), (20, 4)):
         assert not rs.New(k, m).compiled_network(), (k, m)
+    monkeypatch.delenv("BLBRS_BITSLICE")
+    assert [rs.New(k, m).compiled_network() for k, m in ((12, 5), (10, 4), (8, 3), (6, 3), (3, 2))] == \
+        [True, True, True, False, False]
     monkeypatch.setenv("BLBRS_BITSLICE", "0")
-    assert not rs.New(6, 3).compiled_network()
+    assert not rs.New(12, 5).compiled_network()

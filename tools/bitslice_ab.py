@@ -20,7 +20,7 @@ p.add_argument("--reps", type=int, default=3)
 p.add_argument("--iters", type=int, default=5)
 p.add_argument("--ops", default="encode,verify,encode_crc")
 # name:VAR=v+VAR2=w;... -- environment of each variant (read per launch by the library)
-p.add_argument("--variants", default="net:BLBRS_BITSLICE=1;perm:BLBRS_BITSLICE=0")
+p.add_argument("--variants", default="net:BLBRS_BITSLICE=2;perm:BLBRS_BITSLICE=0;policy:BLBRS_BITSLICE=1")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 S = 8 << 20
