@@ -171,7 +171,32 @@ constexpr bool kXcdMap = BLBRS_CRC_XCD != 0;
 constexpr int kStreamThreads = 1024;
 constexpr uint32_t kChunk = 64, kRowBytes = kChunk * 64, kRows = 16;  // 4 KiB rows
 constexpr uint32_t kWaveSeg = kRowBytes * kRows;                      // 64 KiB per wave
-constexpr size_t kStreamLds = kBankedTableBytes;                       // 128 KiB
+// 1 = the row jump S_4032 and the six lane-fold matrices are applied through byte tables in
+// LDS (T_b[v] = the matrix applied to v << 8b: 4 lookups + 2 XOR, about 7 VALU) instead of
+// 32 columns of v_bfe + v_bitop3 (64 VALU on the chain, 15 jumps + 6 folds per 64 KiB).
+#ifndef BLBRS_CRC_TABAPPLY
+#define BLBRS_CRC_TABAPPLY 1
+#endif
+constexpr bool kTabApply = BLBRS_CRC_TABAPPLY != 0;
+constexpr uint32_t kApplyMats = 7;                                     // gap, then wlvl levels 0..5
+constexpr size_t kApplyTabBytes = kApplyMats * 4 * 256 * 4;            // 28 KiB
+constexpr size_t kStreamLds = kBankedTableBytes + (kTabApply ? kApplyTabBytes : 0);  // 156 KiB
+static_assert(kStreamLds <= 160 * 1024, "one workgroup per CU");
+
+// Byte tables of the stream kernel's matrices, after the banked slicing tables.
+__device__ __forceinline__ void init_apply_tables(uint32_t* at, const CrcConsts* c) {
+    for (uint32_t i = threadIdx.x; i < kApplyMats * 1024u; i += kStreamThreads) {
+        const uint32_t mat = i >> 10, b = (i >> 8) & 3u, v = i & 255u;
+        const uint32_t* col = mat == 0 ? c->gap[0] : c->wlvl[0][mat - 1];
+        uint32_t o = 0;
+        for (uint32_t t = 0; t < 8; ++t)
+            if ((v >> t) & 1u) o ^= col[8 * b + t];
+        at[i] = o;
+    }
+}
+__device__ __forceinline__ uint32_t apply_tab(const uint32_t* T, uint32_t r) {
+    return xor3(T[r & 255u], T[256u + ((r >> 8) & 255u)], T[512u + ((r >> 16) & 255u)]) ^ T[768u + (r >> 24)];
+}
 
 struct StreamArgs {
     const uint8_t* data;
@@ -260,15 +285,20 @@ __device__ __forceinline__ Chunk to_lane(const Chunk& in) {
 __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void crc_stream_kernel(
     StreamArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+    uint32_t* const atab = tab + kBankedTableBytes / 4;
     init_banked_tables(tab, a.c, kStreamThreads);
+    if constexpr (kTabApply) init_apply_tables(atab, a.c);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
     const LaneTabs t(lane);
+    // S_4032 (chunk end -> the lane's next chunk) and the lane folds S_{64 * 2^j}.
+    auto jump = [&](uint32_t r) { return kTabApply ? apply_tab(atab, r) : apply(as_const(a.c->gap[0]), r); };
+    auto fold = [&](int j, uint32_t r) {
+        return kTabApply ? apply_tab(atab + 1024u * (1 + j), r) : apply(as_const(&a.c->wlvl[0][j][0]), r);
+    };
     const uint64_t waves = static_cast<uint64_t>(gridDim.x) * (kStreamThreads / 64);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const cu32 gap = as_const(a.c->gap[0]);
-    const cu32 wlvl = as_const(&a.c->wlvl[0][0][0]);
     // Segments in dispatch order, or (BLBRS_CRC_XCD) each XCD's workgroups walking one
     // contiguous eighth of them.
     uint64_t g_lo = blockIdx.x * (kStreamThreads / 64) + wave, g_hi = a.total_segs, g_step = waves;
@@ -343,8 +373,8 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
                     }
                     __builtin_amdgcn_sched_barrier(0);
                     if (r) {
-                        c = apply(gap, c);
-                        cb = apply(gap, cb);
+                        c = jump(c);
+                        cb = jump(cb);
                     }
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
@@ -373,7 +403,7 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
                 if (r + kRing < kRows)
                     ring[r % kRing] = load_row_at(lane_base + (r + kRing) * kRowBytes, row0 + (r + kRing) * kRowBytes, lane);
                 __builtin_amdgcn_sched_barrier(0);
-                if (r) c = apply(gap, c);
+                if (r) c = jump(c);
                 c = crc_chunk(t, c, cur);
             }
             }
@@ -386,7 +416,7 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
                     const uint32_t off = r * kRowBytes + lane * kChunk + 4u * i;
                     w[i] = off >= pad ? *reinterpret_cast<const uint32_t*>(lane_base + r * kRowBytes + 4 * i) : 0u;
                 }
-                c = apply(gap, c);  // no-op on the first row, whose c is 0
+                c = jump(c);  // no-op on the first row, whose c is 0
 #pragma unroll
                 for (int i = 0; i < 16; ++i) c = slice4(t, c ^ w[i]);
             }
@@ -394,7 +424,7 @@ __global__ __launch_bounds__(kStreamThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             const uint32_t other = __shfl_down(c, 1u << j, 64);
-            if ((lane & ((2u << j) - 1u)) == 0) c = apply(wlvl + 32 * j, c) ^ other;
+            if ((lane & ((2u << j) - 1u)) == 0) c = fold(j, c) ^ other;
         }
         if (lane == 0) a.raw[g] = c;
     }
