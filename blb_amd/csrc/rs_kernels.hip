@@ -213,6 +213,9 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
                     for (int u = 0; u < U; ++u) x[c][u] = ld16<NT>(p + u * kStep);
                 }
 #endif
+                // Every load issued before any math: left alone, the scheduler sinks group 1's
+                // loads into group 0's network (fewer registers, less in flight).
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int g = 0; g < U / 2; ++g) {
                     uint32_t xs[K][8], og[MR][8];
