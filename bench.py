@@ -283,7 +283,9 @@ def host_call_extras(k, m, dev, threads=16, seconds=1.0):
 def wide_fused_extras(S, dev):
     """Fused encode+CRC (65532-byte ChecksumFile blocks) against the plain encode of the same
     stripes for blb's widest class RS(12,5) and the bench's RS(10,4), B=512 each, interleaved
-    reps on one stream (rank 0 at N=1 only)."""
+    reps on one stream (rank 0 at N=1 only).  The shipped path runs the compiled bit-plane
+    network; `tables` repeats both on the v_perm table path (BLBRS_BITSLICE=0,
+    read per launch) for comparison with round 2."""
     out = {}
     stream = torch.cuda.current_stream(dev)
     for k, m in ((12, 5), (10, 4)):
@@ -293,20 +295,29 @@ def wide_fused_extras(S, dev):
         e.EncodeBatch(st)
         e.EncodeBatchCRC(st, 65532)
         torch.cuda.synchronize(dev)
-        enc_t, fus_t = [], []
+        times = {}
         for _ in range(3):
-            for fn, acc in ((lambda: e.EncodeBatch(st), enc_t), (lambda: e.EncodeBatchCRC(st, 65532), fus_t)):
-                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s0.record(stream)
-                fn()
-                s1.record(stream)
-                torch.cuda.synchronize(dev)
-                acc.append(s0.elapsed_time(s1))
+            for path, env in (("network", None), ("tables", "0")):
+                if env is not None:
+                    os.environ["BLBRS_BITSLICE"] = env
+                for name, fn in (("encode", lambda: e.EncodeBatch(st)), ("fused", lambda: e.EncodeBatchCRC(st, 65532))):
+                    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s0.record(stream)
+                    fn()
+                    s1.record(stream)
+                    torch.cuda.synchronize(dev)
+                    times.setdefault((path, name), []).append(s0.elapsed_time(s1))
+                os.environ.pop("BLBRS_BITSLICE", None)
         ok = bool(e.VerifyBatch(st).all())
+        ms = {key: float(np.mean(v)) for key, v in times.items()}
+        nbytes = 512 * (k + m) * S
         out[f"encode_crc_fused_rs{k}_{m}_b512"] = {
-            "encode_ms": round(float(np.mean(enc_t)), 3), "fused_ms": round(float(np.mean(fus_t)), 3),
-            "ratio_to_encode": round(float(np.mean(fus_t) / np.mean(enc_t)), 3), "block": 65532,
-            "verify_ok": ok}
+            "encode_ms": round(ms[("network", "encode")], 3), "fused_ms": round(ms[("network", "fused")], 3),
+            "ratio_to_encode": round(ms[("network", "fused")] / ms[("network", "encode")], 3),
+            "fused_frac_of_8TBps": round(nbytes / (ms[("network", "fused")] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "compiled_network": e.compiled_network(),
+            "tables": {"encode_ms": round(ms[("tables", "encode")], 3), "fused_ms": round(ms[("tables", "fused")], 3)},
+            "block": 65532, "verify_ok": ok}
         del st
         torch.cuda.empty_cache()
     return out
@@ -338,7 +349,7 @@ def cold_class_extras(S, dev, batch=512, reps=4):
     g.manual_seed(8303)
     st[:, :k].random_(0, 256, generator=g)
     e = rs.New(k, m)
-    out = {"workload": f"RS(8,3), batch={batch} stripes of {S >> 20} MiB"}
+    out = {"workload": f"RS(8,3), batch={batch} stripes of {S >> 20} MiB", "compiled_network": e.compiled_network()}
 
     def row(name, ms, nbytes, **kw):
         gbs = nbytes / (ms * 1e-3) / 1e9

@@ -8,6 +8,8 @@ BASELINE size, plus calibration kernels of known traffic in the same process:
   verify          VerifyBatch                                   (rs_code_kernel, verify)
   encode_crc      EncodeBatchCRC(65532)                         (encode_crc_tile_kernel + combine)
   crc32c          ChecksumBatch of parity shard k, 65532 blocks (crc_stream_kernel)
+  then RS(12,5) B=512: EncodeBatch and EncodeBatchCRC(65532) on the compiled bit-plane
+  network, and a VerifyBatch of the result
 
 Markers: the dispatch order is fixed; tools/pmc_prod_summary.py matches kernels by name and
 order.  Prints the libblbrs.so sha256 it loaded."""
@@ -50,6 +52,23 @@ torch.cuda.synchronize()
 from blb_amd import checksum  # noqa: E402
 crc1 = checksum.ChecksumBatch(st[:, k], 65532)  # crc32c: parity shard k of every stripe
 torch.cuda.synchronize()
+# blb's widest class on the compiled bit-plane network: encode, then encode fused
+# with the ChecksumFile CRCs
+del st, crc, crc1
+torch.cuda.empty_cache()
+k2, m2, B2 = 12, 5, 512
+st = torch.empty((B2, k2 + m2, S), dtype=torch.uint8, device=dev)
+st[:, :k2].random_(0, 256, generator=g)
+enc2 = rs.New(k2, m2)
+torch.cuda.synchronize()
+enc2.EncodeBatch(st)
+torch.cuda.synchronize()
+crc2 = enc2.EncodeBatchCRC(st, 65532)
+torch.cuda.synchronize()
+ok2 = enc2.VerifyBatch(st)
+torch.cuda.synchronize()
 lib = _lib.LIB_PATH
 print(json.dumps({"lib": lib, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
-                  "verify_ok": bool(ok.all()), "k": k, "m": m, "batch": B, "shard": S}))
+                  "verify_ok": bool(ok.all()), "k": k, "m": m, "batch": B, "shard": S,
+                  "wide": {"k": k2, "m": m2, "batch": B2, "compiled_network": enc2.compiled_network(),
+                           "verify_ok": bool(ok2.all())}}))

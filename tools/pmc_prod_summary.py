@@ -83,6 +83,12 @@ def main():
             ("encode_crc_65532", "encode_crc_tile_kernel", 0, B * (k + m) * S),
             ("encode_crc_combine", "tile_combine_kernel", 0, None),
             ("crc32c_65532", "crc_stream_kernel", 0, B * S)]
+    wide = meta.get("wide")
+    if wide:  # RS(12,5) on the compiled network: dispatches after the RS(6,3) ones
+        wb = wide["batch"] * (wide["k"] + wide["m"]) * S
+        spec += [("encode_rs12_5_network", "rs_code_kernel", 3, wb),
+                 ("encode_crc_rs12_5_network", "encode_crc_tile_kernel", 1, wb),
+                 ("verify_rs12_5_network", "rs_code_kernel", 4, wb)]
     for label, needle, nth, algo in spec:
         f = pick(fetch, needle, nth)
         w = pick(write, needle, nth)
@@ -98,7 +104,7 @@ def main():
             e["lds_bank_conflict_frac"] = round(sqv.get("SQ_LDS_BANK_CONFLICT", 0) / sqv["SQ_LDS_IDX_ACTIVE"], 4)
         kernels[label] = e
     res = {"tag": tag, "commit": commit, "lib_sha256": meta["lib_sha256"],
-           "workload": {"k": k, "m": m, "batch": B, "shard": S},
+           "workload": {"k": k, "m": m, "batch": B, "shard": S, "wide": wide},
            "calibration": {"kernel": copy_f[1], "bytes_each_way": 8 * GIB,
                            "fetch_size_scale": round(f_scale, 4), "write_size_scale": round(w_scale, 4)},
            "hbm_bytes_per_launch": kernels["encode"]["hbm_bytes"],
