@@ -10,6 +10,8 @@
 // leaves the source buffer's pages.  Region heads/tails (< 16 bytes) go byte by byte.
 #include "pack.hpp"
 
+#include <cstdlib>
+
 namespace blbrs {
 namespace {
 
@@ -24,7 +26,11 @@ struct PackArgs {
     uint64_t group_stride; //   + (p % per_group) * dst_stride
 };
 
-constexpr int kUnroll = 4;
+// Lane i receives lane (i + 1) mod 64's dword (DPP wave_rol:1, no LDS).
+__device__ __forceinline__ uint32_t rol1(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x134, 0xF, 0xF, false));
+}
+__device__ __forceinline__ V4 rol1(const V4& v) { return V4{rol1(v.x), rol1(v.y), rol1(v.z), rol1(v.w)}; }
 
 // out = bytes [s, s+16) of the 32-byte window a||b, s = 4q + r (q wave-uniform).
 __device__ __forceinline__ V4 funnel(const V4& a, const V4& b, uint32_t q, uint32_t r) {
@@ -51,9 +57,21 @@ __device__ __forceinline__ V4 funnel(const V4& a, const V4& b, uint32_t q, uint3
     return o;
 }
 
-// Copy n bytes src -> dst with the whole workgroup (n, src, dst uniform).
+template <bool NT>
+__device__ __forceinline__ V4 ld(const V4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// Copy n bytes src -> dst with the whole workgroup (n, src, dst uniform).  Chunk i (16
+// destination bytes) is lane i % 256's, UNR chunks per lane in flight.  A misaligned source is
+// read as aligned blocks: lane i loads block i and takes block i + 1 from the next lane (DPP)
+// -- one load per chunk -- except lane 63 of each wave, whose next block is another wave's and
+// is loaded (DPP = false: every lane loads both blocks, the round-2 kernel).
+template <bool DPP, bool NT, int UNR>
 __device__ void copy_region(uint8_t* dst, const uint8_t* src, uint64_t n) {
     const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
     const uint64_t head = ((16u - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u) < n
                               ? ((16u - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u)
                               : n;
@@ -64,27 +82,44 @@ __device__ void copy_region(uint8_t* dst, const uint8_t* src, uint64_t n) {
     const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s) & 15u);
     const V4* sa = reinterpret_cast<const V4*>(s - mis);  // aligned block holding s[0]
     if (mis == 0) {
-        for (uint64_t c = tid; c < nb; c += kUnroll * kPackThreads) {
-            V4 v[kUnroll];
+        for (uint64_t c = tid; c < nb; c += UNR * kPackThreads) {
+            V4 v[UNR];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u)
-                if (c + u * kPackThreads < nb) v[u] = sa[c + u * kPackThreads];
+            for (int u = 0; u < UNR; ++u)
+                if (c + u * kPackThreads < nb) v[u] = ld<NT>(sa + c + u * kPackThreads);
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u)
+            for (int u = 0; u < UNR; ++u)
                 if (c + u * kPackThreads < nb) __builtin_nontemporal_store(v[u], d + c + u * kPackThreads);
         }
     } else {
         const uint32_t q = mis >> 2, r = mis & 3u;
-        for (uint64_t c = tid; c < nb; c += kUnroll * kPackThreads) {
-            V4 v[kUnroll];
+        // Every block up to nb holds wanted bytes (mis > 0: the last wanted byte lies in block
+        // nb), so no read leaves them.
+        for (uint64_t c = tid; c < nb + (DPP && nb > 0 ? 1 : 0); c += UNR * kPackThreads) {
+            V4 v[UNR], h[UNR];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
+            for (int u = 0; u < UNR; ++u) v[u] = h[u] = V4{0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
                 const uint64_t i = c + u * kPackThreads;
-                if (i < nb) v[u] = funnel(sa[i], sa[i + 1], q, r);  // block i+1 holds wanted bytes
+                if constexpr (DPP) {
+                    if (i <= nb) v[u] = ld<NT>(sa + i);
+                    if (lane == 63u && i < nb) h[u] = ld<NT>(sa + i + 1);
+                } else if (i < nb) {
+                    v[u] = ld<NT>(sa + i);
+                    h[u] = ld<NT>(sa + i + 1);
+                }
             }
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u)
-                if (c + u * kPackThreads < nb) __builtin_nontemporal_store(v[u], d + c + u * kPackThreads);
+            for (int u = 0; u < UNR; ++u) {
+                const uint64_t i = c + u * kPackThreads;
+                V4 hb = h[u];
+                if constexpr (DPP) {
+                    const V4 nx = rol1(v[u]);
+                    if (lane != 63u) hb = nx;
+                }
+                if (i < nb) __builtin_nontemporal_store(funnel(v[u], hb, q, r), d + i);
+            }
         }
     }
     if (tid < tail) {
@@ -104,9 +139,17 @@ __device__ void zero_region(uint8_t* dst, uint64_t n) {
     if (tid < tail) dst[head + (nb << 4) + tid] = 0;
 }
 
+// REMAP: each XCD takes a contiguous eighth of the tiles (blocks are dealt round-robin over
+// the 8 XCDs), so the workgroups resident on one XCD stream neighbouring tiles.
+template <bool DPP, bool NT, int UNR, bool REMAP>
 __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
-    const uint32_t piece = blockIdx.x / a.tiles_per_piece;
-    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x % a.tiles_per_piece) * kPackTile;
+    uint32_t t = blockIdx.x;
+    if constexpr (REMAP) {
+        t = (t % 8u) * (gridDim.x / 8u) + t / 8u;
+        if (t >= a.npieces * a.tiles_per_piece) return;
+    }
+    const uint32_t piece = t / a.tiles_per_piece;
+    const uint64_t t0 = static_cast<uint64_t>(t % a.tiles_per_piece) * kPackTile;
     const uint64_t t1 = t0 + kPackTile < a.piece_len ? t0 + kPackTile : a.piece_len;
     const uint64_t* ex = a.table + a.npieces + 1;
     uint64_t lo = a.table[piece];
@@ -129,7 +172,7 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
         if (off <= cur) {  // inside extent e
             const uint64_t end = off + ex[4 * e + 2] < t1 ? off + ex[4 * e + 2] : t1;
             const uint8_t* src = reinterpret_cast<const uint8_t*>(ex[4 * e]);
-            copy_region(d + cur, src + (cur - off), end - cur);
+            copy_region<DPP, NT, UNR>(d + cur, src + (cur - off), end - cur);
             cur = end > cur ? end : cur;
             ++e;
         } else {  // hole or pad up to the next extent / tile end
@@ -137,6 +180,27 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
             zero_region(d + cur, end - cur);
             cur = end;
         }
+    }
+}
+
+using PackFn = void (*)(PackArgs);
+
+// A/B knob BLBRS_PACK_VARIANT (read per launch): 0 = round-2 kernel (two loads per misaligned
+// chunk, cached loads, 4 chunks per lane in flight, no XCD map), 1 = DPP neighbour + nontemporal
+// loads, 2 = 1 + XCD map, 3 = 2 with 8 chunks per lane in flight, 4 = 2 with 16.
+#ifndef BLBRS_PACK_DEFAULT
+#define BLBRS_PACK_DEFAULT 0
+#endif
+PackFn pick_pack(bool& remap) {
+    const char* e = getenv("BLBRS_PACK_VARIANT");
+    const int v = e ? atoi(e) : BLBRS_PACK_DEFAULT;
+    remap = v >= 2;
+    switch (v) {
+        case 1: return pack_kernel<true, true, 4, false>;
+        case 2: return pack_kernel<true, true, 4, true>;
+        case 3: return pack_kernel<true, true, 8, true>;
+        case 4: return pack_kernel<true, true, 16, true>;
+        default: return pack_kernel<false, false, 4, false>;
     }
 }
 
@@ -153,7 +217,11 @@ hipError_t pack_pieces(uint8_t* dst, uint64_t dst_stride, uint64_t npieces, uint
     }
     PackArgs a{dst, dst_stride, piece_len, static_cast<uint32_t>(npieces), static_cast<uint32_t>(tpp), table_dev,
                per_group, group_stride};
-    hipLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(tpp * npieces)), dim3(kPackThreads), 0, stream, a);
+    bool remap = false;
+    const PackFn fn = pick_pack(remap);
+    uint64_t grid = tpp * npieces;
+    if (remap) grid = (grid + 7) & ~uint64_t{7};  // a multiple of 8 blocks; the extra ones exit
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kPackThreads), 0, stream, a);
     return hipGetLastError();
 }
 

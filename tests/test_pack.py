@@ -156,6 +156,39 @@ def test_gpu_pack_pieces_vs_oracle(piece_len):
 
 
 @gpu
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_gpu_pack_kernel_variants_vs_oracle(monkeypatch, variant):
+    """Every pack_kernel variant (BLBRS_PACK_VARIANT, pack.hip) against the oracle: random
+    extents, plus regions whose 16-byte chunk count sits at the wave and workgroup edges the
+    DPP neighbour exchange depends on (0, 1, 63-65, 255-257, 1023-1025 chunks), from every
+    source misalignment 0..15 and destination offsets that leave heads and tails."""
+    torch = _torch()
+    monkeypatch.setenv("BLBRS_PACK_VARIANT", str(variant))
+    rng = np.random.default_rng(1000 + variant)
+    pool = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
+    dpool = torch.from_numpy(pool).cuda()
+    piece_len = 1_000_003
+    ext = _random_extents(rng, 2, piece_len, pool.size)
+    p, off = 2, 0
+    for chunks in (0, 1, 63, 64, 65, 255, 256, 257, 1023, 1024, 1025):
+        for mis in range(16):
+            ln = 16 * chunks + int(rng.integers(0, 16))
+            head = int(rng.integers(0, 16))
+            if off + head + ln > piece_len:
+                p, off = p + 1, 0
+            src = 16 * int(rng.integers(0, (pool.size - ln - 32) // 16)) + mis
+            ext.append((src, off + head, ln, p))
+            off += head + ln
+    npieces = p + 1
+    dst = torch.full((npieces, piece_len), 0xA5, dtype=torch.uint8, device="cuda")
+    pack.PackPieces(dst, piece_len, [(dpool[s:], o, ln, q) for s, o, ln, q in ext])
+    got = dst.cpu().numpy()
+    for q in range(npieces):
+        want = N.pack_piece(piece_len, [(pool[s:s + ln].tobytes(), o) for s, o, ln, r in ext if r == q])
+        assert got[q].tobytes() == want.ljust(piece_len, b"\0"), q
+
+
+@gpu
 def test_gpu_pack_pinned_sources_and_destination():
     torch = _torch()
     rng = np.random.default_rng(9)
