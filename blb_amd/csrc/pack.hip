@@ -1,6 +1,7 @@
 // pack.hip -- device PackTracts (see pack.hpp).
 //
-// One workgroup per 64 KiB destination tile.  The workgroup finds the first extent of its
+// One workgroup per 64 KiB destination tile, each XCD streaming a contiguous eighth of the
+// tiles, every chunk of the tile in flight at once.  The workgroup finds the first extent of its
 // piece that ends inside or after the tile (binary search over the sorted extents), then
 // walks the tile as a list of uniform regions: "copy from extent e" or "zero".  Inside a
 // region the destination is written as 16-byte aligned dwordx4 stores; the source, which
@@ -185,22 +186,24 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
 
 using PackFn = void (*)(PackArgs);
 
-// A/B knob BLBRS_PACK_VARIANT (read per launch): 0 = round-2 kernel (two loads per misaligned
-// chunk, cached loads, 4 chunks per lane in flight, no XCD map), 1 = DPP neighbour + nontemporal
-// loads, 2 = 1 + XCD map, 3 = 2 with 8 chunks per lane in flight, 4 = 2 with 16.
+// Variants (A/B knob BLBRS_PACK_VARIANT, read per launch; tools/pack_ab.py,
+// profiles/r03/pack/): 6 = the default: XCD map, the whole 64 KiB tile (16 chunks per lane)
+// in flight, cached loads, DPP neighbour block; 0 = the round-2 kernel (two loads per
+// misaligned chunk, 4 chunks per lane, no XCD map); 8 = 6 with nontemporal loads and 8 chunks;
+// 10 = 6 without the DPP exchange.  bench.py's layout, RS(6,3) B=1024 (88 GB): 0 -> 6 = 15.8
+// -> 13.6 ms (6.5 TB/s), distinct sources 16.3 -> 13.9 ms.
 #ifndef BLBRS_PACK_DEFAULT
-#define BLBRS_PACK_DEFAULT 0
+#define BLBRS_PACK_DEFAULT 6
 #endif
 PackFn pick_pack(bool& remap) {
     const char* e = getenv("BLBRS_PACK_VARIANT");
     const int v = e ? atoi(e) : BLBRS_PACK_DEFAULT;
-    remap = v >= 2;
+    remap = v != 0;
     switch (v) {
-        case 1: return pack_kernel<true, true, 4, false>;
-        case 2: return pack_kernel<true, true, 4, true>;
-        case 3: return pack_kernel<true, true, 8, true>;
-        case 4: return pack_kernel<true, true, 16, true>;
-        default: return pack_kernel<false, false, 4, false>;
+        case 0: return pack_kernel<false, false, 4, false>;
+        case 8: return pack_kernel<true, true, 8, true>;
+        case 10: return pack_kernel<false, false, 16, true>;
+        default: return pack_kernel<true, false, 16, true>;
     }
 }
 

@@ -156,7 +156,7 @@ def test_gpu_pack_pieces_vs_oracle(piece_len):
 
 
 @gpu
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 6, 8, 10])
 def test_gpu_pack_kernel_variants_vs_oracle(monkeypatch, variant):
     """Every pack_kernel variant (BLBRS_PACK_VARIANT, pack.hip) against the oracle: random
     extents, plus regions whose 16-byte chunk count sits at the wave and workgroup edges the

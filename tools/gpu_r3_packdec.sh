@@ -11,5 +11,5 @@ timeout -k 10 300 python -u tools/pack_ab.py --reps 3 > "$OUT/pack_ab.json" 2> "
 cut -c1-1500 "$OUT/pack_ab.json"
 timeout -k 10 120 tools/_build/mix_probe dec > "$OUT/mix_dec.txt" 2>&1 || exit $?
 cat "$OUT/mix_dec.txt"
-timeout -k 10 300 python -u tools/dec_ab.py > "$OUT/dec_ab.json" 2> "$OUT/dec_ab.err" || exit $?
+timeout -k 10 300 python -u tools/dec_ab.py --variants "base:;u2:BLBRS_DEC_U=2;u4c:BLBRS_DEC_U=12;u2c:BLBRS_DEC_U=22" > "$OUT/dec_ab.json" 2> "$OUT/dec_ab.err" || exit $?
 cat "$OUT/dec_ab.json"

@@ -18,6 +18,7 @@ p.add_argument("--k", type=int, default=6)
 p.add_argument("--m", type=int, default=3)
 p.add_argument("--batch", type=int, default=1024)
 p.add_argument("--reps", type=int, default=3)
+p.add_argument("--variants", default="", help="fused-call env variants name:VAR=val+...;... (read per launch)")
 a = p.parse_args()
 k, m, B, S = a.k, a.m, a.batch, 8 << 20
 dev = torch.device("cuda:0")
@@ -51,13 +52,33 @@ def timed(fn):
     return s.elapsed_time(e)
 
 
-res = {"fused": [], "pack": [], "encode": []}
+variants = [("fused", {})]
+if a.variants:
+    variants = []
+    for item in a.variants.split(";"):
+        name, _, env = item.partition(":")
+        variants.append((name, dict(kv.split("=", 1) for kv in env.split("+") if kv)))
+knobs = {key for _, env in variants for key in env}
+
+
+def setenv(env):
+    for key in knobs:
+        os.environ.pop(key, None)
+    os.environ.update(env)
+
+
+res = {n: [] for n, _ in variants}
+res.update({"pack": [], "encode": []})
+ok = {}
 for _ in range(a.reps):
-    res["fused"].append(timed(lambda: pack.PackEncode(enc, stripes, ext)))
+    for n, env in variants:
+        setenv(env)
+        res[n].append(timed(lambda: pack.PackEncode(enc, stripes, ext)))
+        ok[n] = bool(enc.VerifyBatch(stripes).all())
+    setenv({})
     res["pack"].append(timed(lambda: pack.PackPieces(tmp.view(B * k, S), S, ext)))
     res["encode"].append(timed(lambda: enc.EncodeBatch(stripes)))
-ok = bool(enc.VerifyBatch(stripes).all())
-fused = min(res["fused"])
+fused = min(min(res[n]) for n, _ in variants)
 print(json.dumps({"k": k, "m": m, "B": B, "ms": {x: [round(v, 3) for v in y] for x, y in res.items()},
-                  "fused_hbm_GBps": round((read_bytes + B * (k + m) * S) / (fused * 1e-3) / 1e9, 1),
+                  "fused_hbm_GBps": {n: round((read_bytes + B * (k + m) * S) / (min(res[n]) * 1e-3) / 1e9, 1) for n, _ in variants},
                   "bytes_read": read_bytes, "verify_ok": ok}))

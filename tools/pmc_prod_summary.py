@@ -63,7 +63,7 @@ def main():
     k, m, B, S = meta["k"], meta["m"], meta["batch"], meta["shard"]
 
     # calibration: the copy kernel that follows the fill (both 8 GiB)
-    big = [x for x in fetch if "rs_code" not in x[1] and "encode_crc" not in x[1] and "crc_stream" not in x[1]]
+    big = [x for x in fetch if not any(n in x[1] for n in ("rs_code", "encode_crc", "crc_stream", "pack_kernel"))]
     copy_f = max(big, key=lambda x: x[2].get("FETCH_SIZE", 0.0))
     f_scale = 8 * GIB / (copy_f[2]["FETCH_SIZE"] * 1024.0)
     bigw = [x for x in write if x[0] == copy_f[0]]
@@ -83,6 +83,8 @@ def main():
             ("encode_crc_65532", "encode_crc_tile_kernel", 0, B * (k + m) * S),
             ("encode_crc_combine", "tile_combine_kernel", 0, None),
             ("crc32c_65532", "crc_stream_kernel", 0, B * S)]
+    if meta.get("pack"):
+        spec.append(("pack_tracts", "pack_kernel", 0, meta["pack"]["bytes_read"] + meta["pack"]["bytes_written"]))
     wide = meta.get("wide")
     if wide:  # RS(12,5) on the compiled network: dispatches after the RS(6,3) ones
         wb = wide["batch"] * (wide["k"] + wide["m"]) * S
