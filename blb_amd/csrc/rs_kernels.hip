@@ -157,11 +157,6 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
     // contiguous eighth of the (stripe, tile) space instead of every 8th tile.
     uint32_t first = blockIdx.x;
     if (a.xcd_remap) first = (first % 8u) * (gridDim.x / 8u) + first / 8u;
-    if (a.xcd_remap == 2) {  // tile-major inside the eighth: column tile j of consecutive stripes
-        const uint32_t per = gridDim.x / 8u, sb = per / a.tiles_per_stripe;
-        const uint32_t x = first / per, r = first - x * per;
-        first = (x * sb + r % sb) * a.tiles_per_stripe + r / sb;
-    }
     for (uint32_t t = first; t < total; t += gridDim.x) {
         const uint32_t b = t / a.tiles_per_stripe;
         const uint64_t tile_off = static_cast<uint64_t>(t - b * a.tiles_per_stripe) * kTile;
@@ -367,11 +362,21 @@ struct Choice {
 };
 
 // Encode / Verify passes of parity rows: the compiled network where the shape has one.
+// A/B knob (read per launch): BLBRS_DEC_U=2 runs one-row stores (a single-erasure
+// ReconstructData, BASELINE config 3) at U = 2 instead of 4.
+int dec_u() {
+    const char* e = getenv("BLBRS_DEC_U");
+    return e ? atoi(e) : 0;
+}
+
 template <int K, int MR, int MODE, int ADDR>
 Choice choice_of(bool cm) {
     constexpr int UC = pick_u_cm(K, MR, MODE);
     if constexpr (K > 0 && UC % 2 == 0 && MODE != 2) {
         if (cm) return {rs_code_kernel<K, MR, MODE, ADDR, UC, kNT, true>, UC, true, true};
+    }
+    if constexpr (K > 0 && MR == 1 && MODE == 0 && pick_u(K, MR, MODE) == 4) {
+        if (dec_u() == 2) return {rs_code_kernel<K, MR, MODE, ADDR, 2, kNT>, 2, true, false};
     }
     return {fn_of<K, MR, MODE, ADDR>(), pick_u(K, MR, MODE), K > 0, false};
 }
@@ -445,10 +450,6 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream) {
         if (total >= 64) {  // one tile per block; a multiple of 8 blocks for the XCD remap
             grid = total & ~uint64_t{7};
             a.xcd_remap = 1;
-            // A/B knob BLBRS_TILE_MAP=2 (read per launch): tile-major order inside each XCD's
-            // eighth; needs whole stripes per eighth (grid == total, B % 8 == 0).
-            const char* tm = getenv("BLBRS_TILE_MAP");
-            if (tm && atoi(tm) == 2 && grid == total && a.B % 8 == 0) a.xcd_remap = 2;
         }
         hipLaunchKernelGGL(ch.fn, dim3(static_cast<unsigned>(grid)), dim3(kThreads), occupancy_lds(ch.cm), stream, a);
         hipError_t e = hipGetLastError();

@@ -25,7 +25,7 @@ struct CodeArgs {
     int32_t rows;             // outputs per stripe (<= kMaxRows)
     int32_t aligned;          // every shard address 16-byte aligned (vector path allowed)
     int32_t* mismatch;        // verify: [B] flags (device)
-    int32_t xcd_remap;        // set by launch_code(): block b starts at tile (b%8)*(grid/8) + b/8 (2: then tile-major inside that eighth)
+    int32_t xcd_remap;        // set by launch_code(): block b starts at tile (b%8)*(grid/8) + b/8
     int32_t nstore;           // kStoreVerify: rows [0, nstore) are stored, the rest compared
     int32_t parity;           // rows = encode parity rows 0..rows-1 of k: the compiled network
                               //   (gf_bitslice.hpp) where the shape has one
