@@ -31,7 +31,6 @@
 #include "rs_kernels.hpp"
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "gf_bitslice.hpp"
 #include "gf_device.hpp"
@@ -362,21 +361,11 @@ struct Choice {
 };
 
 // Encode / Verify passes of parity rows: the compiled network where the shape has one.
-// A/B knob (read per launch): BLBRS_DEC_U=2 runs one-row stores (a single-erasure
-// ReconstructData, BASELINE config 3) at U = 2 instead of 4.
-int dec_u() {
-    const char* e = getenv("BLBRS_DEC_U");
-    return e ? atoi(e) : 0;
-}
-
 template <int K, int MR, int MODE, int ADDR>
 Choice choice_of(bool cm) {
     constexpr int UC = pick_u_cm(K, MR, MODE);
     if constexpr (K > 0 && UC % 2 == 0 && MODE != 2) {
         if (cm) return {rs_code_kernel<K, MR, MODE, ADDR, UC, kNT, true>, UC, true, true};
-    }
-    if constexpr (K > 0 && MR == 1 && MODE == 0 && pick_u(K, MR, MODE) == 4) {
-        if (dec_u() == 2) return {rs_code_kernel<K, MR, MODE, ADDR, 2, kNT>, 2, true, false};
     }
     return {fn_of<K, MR, MODE, ADDR>(), pick_u(K, MR, MODE), K > 0, false};
 }
