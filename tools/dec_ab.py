@@ -1,5 +1,6 @@
 """A/B of the single-erasure ReconstructData launch (BASELINE config 3: RS(6,3), B=1024 x
-8 MiB, data shard 1 missing): env variants read per launch (e.g. BLBRS_DEC_U=2, rs_kernels.hip),
+8 MiB, data shard 1 missing): env variants read per launch (the BLBRS_DEC_U knob of the A/B build
+behind profiles/r03/dec/ is not kept),
 interleaved reps in one process on the same buffers; the rebuilt shard must equal the original
 under every variant."""
 import argparse
@@ -17,7 +18,7 @@ p.add_argument("--k", type=int, default=6)
 p.add_argument("--m", type=int, default=3)
 p.add_argument("--batch", type=int, default=1024)
 p.add_argument("--reps", type=int, default=5)
-p.add_argument("--variants", default="base:;u2:BLBRS_DEC_U=2",
+p.add_argument("--variants", default="shipped:;tables:BLBRS_BITSLICE=0",
                help="name:VAR=val+VAR=val;... (empty = defaults)")
 a = p.parse_args()
 k, m, B, S = a.k, a.m, a.batch, 8 << 20

@@ -1,4 +1,4 @@
-"""A/B of coding-kernel launch knobs read per launch (e.g. BLBRS_TILE_MAP=2, rs_kernels.hip):
+"""A/B of coding-kernel launch knobs read per launch (e.g. BLBRS_BITSLICE=0, gf_bitslice.hpp):
 EncodeBatch, VerifyBatch and a 1-erasure ReconstructBatch of RS(k,m), B stripes of 8 MiB,
 device-resident, every variant interleaved per rep in one process on the same buffers.
 Parity under every variant must equal the first variant's; Verify must pass and the rebuilt
@@ -19,7 +19,7 @@ p.add_argument("--m", type=int, default=3)
 p.add_argument("--batch", type=int, default=1024)
 p.add_argument("--reps", type=int, default=5)
 p.add_argument("--ops", default="encode,verify,reconstruct_data1")
-p.add_argument("--variants", default="base:;tm2:BLBRS_TILE_MAP=2", help="name:VAR=val+VAR=val;...")
+p.add_argument("--variants", default="shipped:;tables:BLBRS_BITSLICE=0", help="name:VAR=val+VAR=val;...")
 a = p.parse_args()
 k, m, B, S = a.k, a.m, a.batch, 8 << 20
 dev = torch.device("cuda:0")
