@@ -18,7 +18,7 @@ p.add_argument("--k", type=int, default=6)
 p.add_argument("--m", type=int, default=3)
 p.add_argument("--batch", type=int, default=1024)
 p.add_argument("--reps", type=int, default=5)
-p.add_argument("--variants", default="shipped:;tables:BLBRS_BITSLICE=0",
+p.add_argument("--variants", default="shipped:",
                help="name:VAR=val+VAR=val;... (empty = defaults)")
 a = p.parse_args()
 k, m, B, S = a.k, a.m, a.batch, 8 << 20
