@@ -82,15 +82,39 @@ def pmc_traffic(k, m, batch, shard):
     return None, None
 
 
+def cgroup_cpu_quota():
+    """The job's CPU quota in cores from the cgroup (v2 cpu.max, else v1 cfs quota/period);
+    None when unlimited or unreadable, with the raw text."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            raw = open(path).read().strip()
+            q, per = raw.split()[:2]
+            return (None if q == "max" else round(int(q) / int(per), 2)), f"{path}: {raw}"
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return (None if q < 0 else round(q / per, 2)), f"cgroup v1 cfs_quota_us={q} cfs_period_us={per}"
+    except (OSError, ValueError):
+        return None, "no cgroup cpu quota file"
+
+
 def cpu_baseline(k, m, seconds):
     """klauspost's algorithm (AVX2 vpshufb nibble tables, OpenMP byte-range split like
-    codeSomeShardsP) from the oracle restatement, on a bounded sample of the workload."""
+    codeSomeShardsP) from the oracle restatement, on a bounded sample of the workload.  Records
+    what bounds the thread count (affinity, OMP_NUM_THREADS, cgroup quota), the rate per thread
+    and a 1/2/4/8/16-thread sweep up to the job's share, so the figure can be scaled to a whole
+    host."""
     from oracle import oracle as O
     # Every core this process may run on (its affinity mask), capped by OMP_NUM_THREADS where
-    # the GPU box sets it to the job's CPU share.
+    # the GPU box sets it to the job's CPU share, and by the cgroup quota.
     affinity = len(os.sched_getaffinity(0))
     omp = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    quota, quota_src = cgroup_cpu_quota()
     threads = max(1, min(affinity, omp) if omp else affinity)
+    if quota is not None:
+        threads = max(1, min(threads, int(quota)))
     cpu_model = "unknown"
     try:
         for ln in open("/proc/cpuinfo"):
@@ -117,8 +141,24 @@ def cpu_baseline(k, m, seconds):
         if el >= seconds:
             break
     gibps = done * k * TRACT / GIB / el
+    # Thread sweep (1.5 s per point) on the same stripes: how the rate scales with cores.
+    sweep = {}
+    for t in (1, 2, 4, 8, 16):
+        if t > threads:
+            break
+        n, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < 1.5:
+            data, par = stripes[n % nstripes]
+            O.code(rows, data, par, use_avx2=True, threads=t)
+            n += 1
+        sweep[str(t)] = round(n * k * TRACT / GIB / (time.perf_counter() - t1), 2)
     out = {"value": round(gibps, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "per_thread_GiBps": round(gibps / threads, 3),
+           "thread_sweep_GiBps": sweep,
+           "scaling_note": "per_thread_GiBps x a host's cores is an upper bound; the sweep shows how far "
+                           "from linear the rate already is at the job's share",
            "nproc": affinity, "os_cpu_count": os.cpu_count(), "omp_num_threads": omp or None,
+           "cgroup_cpu_quota_cores": quota, "cgroup_cpu_quota_source": quota_src,
            "cpu_model": cpu_model, "avx2": bool(O.lib().rso_have_avx2()),
            "sample": f"RS({k},{m}) encode of {done} stripes x {k}x8MiB "
                      f"({done * k * TRACT / GIB:.1f} GiB data, {el:.1f} s) by the oracle's "
@@ -230,9 +270,10 @@ def scale_extras(enc, k, m, S, world, rank, dev, dist):
 
 def host_call_extras(k, m, dev, threads=16, seconds=1.0):
     """The tractserver's real call shape (rank 0 at N=1): `threads` concurrent RSEncode RPCs,
-    each calling Encode on one 4 MiB increment (EncodeIncrementSize, store.go:1099) of pool
-    buffers (rpc.GetBuffer -> blbrs_buffer_get, pinned, coded in place over PCIe), per call and
-    through a Batcher (window 0).  PCIe-inclusive; never the bench value."""
+    each calling Encode on one 4 MiB increment (EncodeIncrementSize, store.go:1099) of
+    library-owned pinned buffers (blbrs_buffer_get, allocated once and reused, coded in place
+    over PCIe), per call and through a Batcher (window 0).  `rpc_pool_churn` is the path blb
+    would actually run (rpc_pool_extras).  PCIe-inclusive; never the bench value."""
     import threading
     S = 4 << 20
     out = {"threads": threads, "increment_bytes": S}
@@ -280,12 +321,65 @@ def host_call_extras(k, m, dev, threads=16, seconds=1.0):
     return out
 
 
+def rpc_pool_extras(k, m, dev, threads=16, seconds=1.0, gc_every=(0, 64, 8)):
+    """rpc.GetBuffer as blb's drop-in pool builds it (blb_amd/rpc.py = go/rsgpu's GetBuffer):
+    caller-owned class buffers registered with the engine on creation and unregistered when
+    collected.  Each of `threads` RPC threads takes k + m 4 MiB buffers per call with
+    GetBuffer, Encodes, and PutBuffers them; every `gc_every` calls per thread it runs rpc.gc()
+    (what a Go GC cycle does to a sync.Pool: the idle buffers are dropped, so later calls
+    register fresh ones).  0 = no GC.  Reports GiB/s of data, the registrations and the mean
+    hipHostRegister / hipHostUnregister wall time per 4 MiB buffer under concurrent coding."""
+    import threading
+    from blb_amd import rpc
+    S = 4 << 20
+    out = {"threads": threads, "increment_bytes": S}
+    enc = rs.New(k, m, devices=[dev.index])
+    g = np.random.default_rng(5)
+    data = [g.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+    for every in gc_every:
+        rpc.gc()
+        base = dict(rpc.stats)
+        counts = [0] * threads
+        stop = time.perf_counter() + seconds
+
+        def loop(t):
+            n = 0
+            while time.perf_counter() < stop:
+                sh = [rpc.GetBuffer(S) for _ in range(k + m)]
+                for i in range(k):
+                    sh[i][:] = data[i]
+                enc.Encode(sh)
+                for b in sh:
+                    rpc.PutBuffer(b)
+                n += 1
+                if every and n % every == 0:
+                    rpc.gc()
+            counts[t] = n
+
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=loop, args=(t,)) for t in range(threads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        el = time.perf_counter() - t0
+        d = {key: rpc.stats[key] - base[key] for key in base}
+        out[f"gc_every_{every or 'never'}"] = {
+            "GiBps_data": round(sum(counts) * k * S / GIB / el, 2), "calls": sum(counts),
+            "registrations": d["registered"] + d["reregistered"], "unregistrations": d["unregistered"],
+            "refused": d["refused"],
+            "register_ms_mean": round(1e3 * d["register_s"] / max(1, d["registered"] + d["reregistered"]), 3),
+            "unregister_ms_mean": round(1e3 * d["unregister_s"] / max(1, d["unregistered"]), 3)}
+    rpc.gc()
+    return out
+
+
 def wide_fused_extras(S, dev):
     """Fused encode+CRC (65532-byte ChecksumFile blocks) against the plain encode of the same
     stripes for blb's widest class RS(12,5) and the bench's RS(10,4), B=512 each, interleaved
     reps on one stream (rank 0 at N=1 only).  The shipped path runs the compiled bit-plane
-    network; `tables` repeats both on the v_perm table path (BLBRS_BITSLICE=0,
-    read per launch) for comparison with round 2."""
+    network; `tables` repeats both on the v_perm table path (knob BLBRS_BITSLICE=0)
+    for comparison with round 2."""
     out = {}
     stream = torch.cuda.current_stream(dev)
     for k, m in ((12, 5), (10, 4)):
@@ -297,17 +391,15 @@ def wide_fused_extras(S, dev):
         torch.cuda.synchronize(dev)
         times = {}
         for _ in range(3):
-            for path, env in (("network", None), ("tables", "0")):
-                if env is not None:
-                    os.environ["BLBRS_BITSLICE"] = env
-                for name, fn in (("encode", lambda: e.EncodeBatch(st)), ("fused", lambda: e.EncodeBatchCRC(st, 65532))):
-                    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    s0.record(stream)
-                    fn()
-                    s1.record(stream)
-                    torch.cuda.synchronize(dev)
-                    times.setdefault((path, name), []).append(s0.elapsed_time(s1))
-                os.environ.pop("BLBRS_BITSLICE", None)
+            for path, knobs in (("network", {}), ("tables", {"BLBRS_BITSLICE": 0})):
+                with rs.tuning(**knobs):
+                    for name, fn in (("encode", lambda: e.EncodeBatch(st)), ("fused", lambda: e.EncodeBatchCRC(st, 65532))):
+                        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        s0.record(stream)
+                        fn()
+                        s1.record(stream)
+                        torch.cuda.synchronize(dev)
+                        times.setdefault((path, name), []).append(s0.elapsed_time(s1))
         ok = bool(e.VerifyBatch(st).all())
         ms = {key: float(np.mean(v)) for key, v in times.items()}
         nbytes = 512 * (k + m) * S
@@ -332,6 +424,96 @@ def _ev_ms(fn, reps, stream, dev):
         e.record(stream)
     torch.cuda.synchronize(dev)
     return float(np.mean([s.elapsed_time(e) for s, e in evs]))
+
+
+def _stream_probe():
+    """tools/_build/libstream_probe.so (the access-pattern probe), or None when not built."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "_build", "libstream_probe.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.stream_probe.restype = ctypes.c_int
+    lib.stream_probe.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] + [ctypes.c_size_t] * 4 + [ctypes.c_void_p]
+    return lib
+
+
+def recovery_extras(S, dev, reps=3):
+    """blb's real recovery call shapes for every storage class (rank 0 at N=1), B chosen so each
+    batch is ~64-72 GiB of HBM:
+
+    * rpc_{e}bad -- the curator's recovery RPC (internal/curator/reconstruct.go:51-79 ->
+      internal/tractserver/store.go:1062-1102): the tractserver reads exactly the first k good
+      pieces and Reconstruct rebuilds ALL m absent slots (the e bad pieces and the good parity
+      pieces it did not read); the Verify after it has nothing left to compare.  e = 1 and m.
+    * client_rows{r} -- the client's degraded read (client/blb/reconstruct.go:137-173): the
+      first k good replies, ReconstructData of the r missing data slots (r = 1: every other
+      data piece answered; r = m: the parity pieces answered first).
+
+    Each row: the shipped path's HIP-event time (a run-time decode network where it applies,
+    DESIGN §4h, else the v_perm tables), the tables alone, algorithmic bytes B*(k+rows)*S and
+    the fraction of 8 TB/s, and the trivial-XOR stream of the same reads and writes in the same
+    layout and launch shape (tools/stream_probe.hip) at the kernel's U and at its best U."""
+    probe = _stream_probe()
+    stream = torch.cuda.current_stream(dev)
+    out = {"note": "ms = median of interleaved reps; probe = trivial-XOR stream, same bytes/layout/launch"}
+    for k, m, B in ((6, 3, 1024), (8, 3, 768), (10, 3, 640), (12, 5, 480)):
+        n = k + m
+        st = torch.empty((B, n, S), dtype=torch.uint8, device=dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(97531 + k)
+        st[:, :k].random_(0, 256, generator=g)
+        e = rs.New(k, m)
+        e.EncodeBatch(st)
+        spread = [1 + (i * k) // m for i in range(m)]
+        rows = []
+        for nbad in (1, m):
+            good = [i for i in range(n) if i not in spread[:nbad]]
+            rows.append((f"rpc_{nbad}bad", [i in good[:k] for i in range(n)], False, m))
+        rows.append(("client_rows1", [i != 1 and i <= k for i in range(n)], True, 1))
+        first_k = [j for j in range(n) if j not in spread][:k]
+        rows.append((f"client_rows{m}", [i in first_k for i in range(n)], True, m))
+        cls = {}
+        for name, present, data_only, nrows in rows:
+            targets = [i for i in range(n) if not present[i] and (i < k or not data_only)]
+            ref = {i: st[:, i].clone() for i in targets if i < k}
+            for i in targets:
+                st[:, i].fill_(0xA5)
+            e.ReconstructBatch(st, present, data_only=data_only)  # requests the network
+            torch.cuda.synchronize(dev)
+            exact = all(bool(torch.equal(st[:, i], r)) for i, r in ref.items())
+            if not data_only:
+                exact = exact and bool(e.VerifyBatch(st).all())
+            del ref
+            rs.rtc_wait()
+            u = 4 if k + nrows <= 9 else 2
+            fns = {"shipped": lambda: e.ReconstructBatch(st, present, data_only=data_only),
+                   "tables": lambda: e.ReconstructBatch(st, present, data_only=data_only)}
+            if probe is not None:
+                for pu in (1, 2, 4):
+                    fns[f"probe_u{pu}"] = (lambda pu=pu: probe.stream_probe(
+                        k, nrows, pu, st.data_ptr(), S, n * S, B, S, stream.cuda_stream))
+            times = {key: [] for key in fns}
+            for _ in range(reps):
+                for key, fn in fns.items():
+                    with rs.tuning(**({"BLBRS_RTC": 0} if key == "tables" else {})):
+                        times[key].append(_ev_ms(fn, 1, stream, dev))
+            e.EncodeBatch(st)  # the probe wrote garbage over parity shards [k, k + rows): restore them
+            ms = {key: sorted(v)[len(v) // 2] for key, v in times.items()}
+            nbytes = B * (k + nrows) * S
+            row = {"rows": nrows, "present": [i for i in range(n) if present[i]], "algorithmic_bytes": nbytes,
+                   "ms": round(ms["shipped"], 3), "frac_of_8TBps": round(nbytes / (ms["shipped"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "tables_ms": round(ms["tables"], 3), "network": rs.rtc_eligible(k, nrows), "bit_exact": exact}
+            if probe is not None:
+                best = min(ms[f"probe_u{pu}"] for pu in (1, 2, 4))
+                row.update({"probe_ms_same_u": round(ms[f"probe_u{u}"], 3), "probe_ms_best_u": round(best, 3),
+                            "ratio_to_probe": round(ms["shipped"] / best, 4)})
+            cls[name] = row
+        out[f"RS({k},{m})_B{B}"] = cls
+        del st
+        torch.cuda.empty_cache()
+    out["rtc"] = rs.rtc_stats()
+    return out
 
 
 def cold_class_extras(S, dev, batch=512, reps=4):
@@ -418,6 +600,9 @@ def main():
     local = local % max(1, torch.cuda.device_count())  # identity on a node with >= N GPUs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # NUMA: this rank's CPUs and future host pages on its GPU's node (2 sockets x 4 GPUs on an
+    # 8-GPU host), before any pin_memory (config 5's pinned stripes, the pool buffers).
+    numa = multigpu.bind_to_node(rs.device_numa_node(local))
     # One process per GPU: this rank's host-memory calls (config 5) stay on its own GPU
     # instead of spreading over every visible device (the library's in-process default).
     rs.set_default_devices([local])
@@ -513,13 +698,15 @@ def main():
         extra["verify"] = {"GiBps_data": round(B * k * S / GIB / (ver_ms * 1e-3), 2),
                            "ms_per_launch": round(ver_ms, 3), "all_ok": flags_ok,
                            "hbm_GBps_algorithmic": round(B * (k + m) * S / (ver_ms * 1e-3) / 1e9, 1)}
-        # reconstructAndVerify (store.go:1132-1142, the recovery RPC): Reconstruct of data
-        # shard 1 then Verify as two passes, against the one-pass store+verify kernel.
+        # reconstructAndVerify (store.go:1132-1142) with all 8 survivors present: Reconstruct of
+        # data shard 1 then Verify as two passes, against the one-pass store+verify kernel.  NOT
+        # blb's RPC shape (the RPC passes exactly k survivors, so its Verify is vacuous):
+        # `recovery_shapes` has that.
         rv_two = _ev_ms(lambda: (enc.ReconstructBatch(stripes, present), enc.VerifyBatch(stripes)),
                         max(3, a.steps // 4), stream, dev)
         rv_ok = bool(enc.ReconstructAndVerifyBatch(stripes, present).all())
         rv_one = _ev_ms(lambda: enc.ReconstructAndVerifyBatch(stripes, present), max(3, a.steps // 4), stream, dev)
-        extra["reconstruct_and_verify_1_data_erasure"] = {
+        extra["reconstruct_and_verify_8_present_1_data_erasure"] = {
             "one_pass_ms": round(rv_one, 3), "two_pass_ms": round(rv_two, 3), "speedup": round(rv_two / rv_one, 3),
             "hbm_GBps_algorithmic_one_pass": round(algo_bytes / (rv_one * 1e-3) / 1e9, 1), "verify_ok": rv_ok}
         # CRC-32C of every parity shard in 65532-byte ChecksumFile blocks (§8f row 2).
@@ -540,7 +727,7 @@ def main():
                                          "ms": round(crc_ms, 3), "bytes": B * m * S, "block": 65532}
         # The same two steps fused: parity checksummed in registers.  Default = the tile-grid
         # kernel (encode_crc_tile.hip); the persistent segment kernel (encode_crc.hip) is
-        # timed beside it for the A/B (BLBRS_EC_PERSISTENT, read per call).
+        # timed beside it for the A/B (knob BLBRS_EC_PERSISTENT).
         def fused_ms(blk):
             enc.EncodeBatchCRC(stripes, blk)
             torch.cuda.synchronize(dev)
@@ -554,11 +741,8 @@ def main():
             return float(np.mean([s.elapsed_time(e) for s, e in f_evs]))
         for blk_name, blk in (("blocks65532", checksum.CHECKSUM_BLOCK_DATA), ("whole_shard", 0)):
             f_ms = fused_ms(blk)
-            os.environ["BLBRS_EC_PERSISTENT"] = "1"
-            try:
+            with rs.tuning(BLBRS_EC_PERSISTENT=1):
                 p_ms = fused_ms(blk)
-            finally:
-                del os.environ["BLBRS_EC_PERSISTENT"]
             extra[f"encode_crc_fused_{blk_name}"] = {
                 "ms_per_launch": round(f_ms, 3), "GiBps_data": round(B * k * S / GIB / (f_ms * 1e-3), 2),
                 "ratio_to_encode": round(f_ms / launch_ms, 3),
@@ -631,7 +815,9 @@ def main():
         if world == 1:
             extra.update(wide_fused_extras(S, dev))
             extra["cold_class_rs83_b512"] = cold_class_extras(S, dev)
+            extra["recovery_shapes"] = recovery_extras(S, dev)
             extra["host_calls_rs63_encode_4MiB_pool"] = host_call_extras(k, m, dev)
+            extra["host_calls_rs63_encode_4MiB_rpc_pool_churn"] = rpc_pool_extras(k, m, dev)
     if rank == 0 and world == 1 and not a.no_extra:
         cpu = cpu_baseline(k, m, a.cpu_seconds)
 
@@ -662,6 +848,7 @@ def main():
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "traffic": traffic, "traffic_source": traffic_src},
             "cpu_baseline": cpu,
+            "numa": numa,
             "verify_ok": ok,
         }
         if extra:

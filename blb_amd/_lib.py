@@ -70,6 +70,16 @@ SIGNATURES = {
     "blbrs_trim": (_I, []),
     "blbrs_set_device": (_I, [_I]),
     "blbrs_device_count": (_I, [ctypes.POINTER(_I)]),
+    "blbrs_device_numa_node": (_I, [_I, ctypes.POINTER(_I)]),
+    "blbrs_set_device_numa_node": (_I, [_I, _I]),
+    "blbrs_host_numa_node": (_I, [_P, ctypes.POINTER(_I)]),
+    "blbrs_lane_policy": (_I, [_P, _P, _SZ, _SZ, _I, ctypes.POINTER(_SZ)]),
+    "blbrs_set_tuning": (_I, [ctypes.c_char_p, ctypes.c_long]),
+    "blbrs_get_tuning": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_long)]),
+    "blbrs_rtc_get_stats": (_I, [_P]),
+    "blbrs_rtc_compile": (_I, [_I, _I, _P, _I, _I]),
+    "blbrs_rtc_wait": (_I, [ctypes.c_long]),
+    "blbrs_rtc_network_source": (_I, [_I, _I, _P, _I, _P, _SZ, ctypes.POINTER(_I)]),
     "blbrs_last_error": (ctypes.c_char_p, []),
     "blbrs_version": (ctypes.c_char_p, []),
     "blbrs_strerror": (ctypes.c_char_p, [_I]),
@@ -95,6 +105,12 @@ class LaneStats(ctypes.Structure):
     """blbrs_lane_stats"""
     _fields_ = [("calls", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("inflight_calls", ctypes.c_int64),
                 ("inflight_bytes", ctypes.c_int64)]
+
+
+class RtcStats(ctypes.Structure):
+    """blbrs_rtc_stats"""
+    _fields_ = [("requested", ctypes.c_uint64), ("compiled", ctypes.c_uint64), ("loaded", ctypes.c_uint64),
+                ("failed", ctypes.c_uint64), ("pending", ctypes.c_uint64), ("compile_ms", ctypes.c_double)]
 
 
 class DevPart(ctypes.Structure):

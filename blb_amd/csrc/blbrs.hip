@@ -39,7 +39,9 @@
 #include "gf_bitslice.hpp"
 #include "pack.hpp"
 #include "rs_kernels.hpp"
+#include "rtc.hpp"
 #include "runtime.hpp"
+#include "tuning.hpp"
 
 using namespace blbrs;
 using rt::aligned16;
@@ -62,6 +64,7 @@ struct Pass {
     bool parity = false;  // rows = encode parity rows 0..rows-1 of k_in (compiled network)
     std::vector<int32_t> in_idx, out_idx;
     std::vector<uint32_t> tables;
+    Mat coef;  // rows x k_in coefficients (a run-time network is generated from them, rtc.hpp)
 };
 
 // Host description of an operation: rows x k_in coefficients, split into passes.
@@ -88,6 +91,7 @@ void split_passes(HostPlan& p) {
                 p.rows.begin() + static_cast<size_t>(r0 + ps.rows) * p.k_in);
         ps.tables = perm_tables(sub, ps.rows, p.k_in);
         ps.parity = bs::is_parity_rows(sub.data(), ps.rows, p.k_in);
+        ps.coef = std::move(sub);
         p.passes.push_back(std::move(ps));
     }
 }
@@ -101,6 +105,8 @@ struct DevPass {
     int k_in = 0, rows = 0;
     int nstore = -1;
     bool parity = false;
+    Mat coef;
+    std::shared_ptr<rtc::NetSlot> net;  // run-time network lookups of this pass (rtc.hpp)
 };
 struct DevPlan {
     std::vector<DevPass> passes;
@@ -123,6 +129,8 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
         d.rows = ps.rows;
         d.nstore = ps.nstore;
         d.parity = ps.parity;
+        d.coef = ps.coef;
+        d.net = std::make_shared<rtc::NetSlot>();
         const size_t n_in = ps.in_idx.size() * 4, n_out = round_up(ps.out_idx.size() * 4, 16);
         const size_t off_out = round_up(n_in, 16), off_tab = off_out + n_out;
         const size_t bytes = off_tab + ps.tables.size() * 4;
@@ -376,7 +384,22 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
             a.nstore = ps.nstore;
             m = ps.nstore == ps.rows ? Mode::kStore : ps.nstore == 0 ? Mode::kVerify : Mode::kStoreVerify;
         }
-        hipError_t e = launch_code(a, m, stream);
+        // Wide passes the library has no compiled network for (decode rows; encode rows of k
+        // outside the compiled list) take a network generated for their coefficients once it is
+        // loaded; until then, and on failure, the table kernel.
+        const rtc::NetKernel* net = nullptr;
+        const bool aot = bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode) &&  // compiled encode network
+                         tune::get(tune::kRtcEncode) == 0;
+        if (!aot && bs::mode() != 0 && rtc::eligible(ps.k_in, ps.rows)) {
+            auto& slot = ps.net->k[static_cast<int>(m)][st.base ? 0 : 1];
+            rtc::NetKernel* nk = slot.load(std::memory_order_acquire);
+            if (!nk) {
+                nk = rtc::request(plan.device, ps.k_in, ps.rows, m, st.base != nullptr, ps.coef.data());
+                slot.store(nk, std::memory_order_release);
+            }
+            net = nk;
+        }
+        hipError_t e = launch_code(a, m, stream, net);
         if (e != hipSuccess) return hip_fail(e, "launch rs_code_kernel");
     }
     return BLBRS_OK;
@@ -612,7 +635,12 @@ int host_call(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const
     }
     int occ = 0;
     if (dev < 0) {
-        const size_t li = rt::pick_lane(lanes, enc->rr);
+        // Host shards: prefer a GPU on the NUMA node holding them (pool and registered buffers
+        // know their node; pageable memory gives no preference).
+        int node = -1;
+        for (int i = 0; i < n && node < 0; ++i)
+            if (shards[i]) node = rt::host_numa_node(shards[i]);
+        const size_t li = rt::pick_lane(lanes, enc->rr, node);
         dev = lanes[li];
         occ = rt::lane_keys(lanes)[li].second;
     }
@@ -1062,9 +1090,71 @@ int blbrs_parity_shards(const blbrs_encoder* enc) { return enc ? enc->m : 0; }
 int blbrs_encoder_compiled_network(const blbrs_encoder* enc) {
     if (!enc) return 0;
     const auto hp = enc->core->encode_plan();
-    for (const Pass& ps : hp->passes)
-        if (!bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode)) return 0;
-    return 1;
+    int code = 1, tile = 1, pack = 1, rtc_net = 1;
+    for (const Pass& ps : hp->passes) {
+        code &= bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode) ? 1 : 0;
+        tile &= bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideTile) ? 1 : 0;
+        pack &= bs::use(ps.parity, ps.k_in, ps.rows, bs::kWidePack) ? 1 : 0;
+        rtc_net &= !bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode) && bs::mode() != 0 &&
+                   rtc::eligible(ps.k_in, ps.rows) ? 1 : 0;
+    }
+    return (code ? BLBRS_NET_CODE : 0) | (tile ? BLBRS_NET_TILE : 0) | (pack ? BLBRS_NET_PACK : 0) |
+           (rtc_net ? BLBRS_NET_RTC : 0);
+}
+
+int blbrs_device_numa_node(int device, int* node) {
+    if (!node || device < 0) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
+    *node = rt::device_numa_node(device);
+    return BLBRS_OK;
+}
+
+int blbrs_set_device_numa_node(int device, int node) { return rt::set_device_numa_node(device, node); }
+
+int blbrs_host_numa_node(const void* p, int* node) {
+    if (!node) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    *node = rt::host_numa_node(p);
+    return BLBRS_OK;
+}
+
+int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t start, int node, size_t* lane) {
+    if (!nodes || !loads || !lane || n == 0 || start >= n) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
+    *lane = rt::pick_lane_policy(nodes, loads, n, start, node);
+    return BLBRS_OK;
+}
+
+int blbrs_rtc_get_stats(blbrs_rtc_stats* out) {
+    if (!out) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    const rtc::Stats s = rtc::stats();
+    out->requested = s.requested;
+    out->compiled = s.compiled;
+    out->loaded = s.loaded;
+    out->failed = s.failed;
+    out->pending = s.pending;
+    out->compile_ms = s.compile_ms;
+    return BLBRS_OK;
+}
+
+int blbrs_rtc_compile(int k, int rows, const uint8_t* coef, int mode, int strided) {
+    if (k < 1 || k > 16 || rows < 1 || rows > kMaxRows || !coef || mode < 0 || mode > 2)
+        return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
+    std::string log;
+    if (!rtc::compile_only(k, rows, static_cast<Mode>(mode), strided != 0, coef, &log))
+        return fail(BLBRS_ERR_HIP, "hipRTC: " + log.substr(0, 2000));
+    return BLBRS_OK;
+}
+
+int blbrs_rtc_wait(long timeout_ms) {
+    return rtc::wait_idle(timeout_ms) ? BLBRS_OK : fail(BLBRS_ERR_LIMIT, "run-time networks still compiling");
+}
+
+int blbrs_rtc_network_source(int k, int rows, const uint8_t* coef, int cse, char* out, size_t cap, int* ops) {
+    if (k < 1 || rows < 1 || k > 256 || rows > 256 || !coef || !out) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
+    int n = 0;
+    const std::string src = rtc::network_source(k, rows, coef, cse != 0, &n);
+    if (src.size() + 1 > cap) return fail(BLBRS_ERR_INVALID_ARG, "buffer too small");
+    std::memcpy(out, src.c_str(), src.size() + 1);
+    if (ops) *ops = n;
+    return BLBRS_OK;
 }
 
 int blbrs_matrix(const blbrs_encoder* enc, uint8_t* out, size_t cap) {
@@ -1583,7 +1673,7 @@ int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {
     uint64_t view = 0;
     int owner = -1;
     const bool visible = rt::device_view(data, &view, &owner);
-    const int dev = owner >= 0 ? owner : lanes[rt::pick_lane(lanes, rr)];
+    const int dev = owner >= 0 ? owner : lanes[rt::pick_lane(lanes, rr, rt::host_numa_node(data))];
     rt::LoadTicket ticket;
     ticket.take(dev, 0, len);
     rt::DeviceGuard guard;

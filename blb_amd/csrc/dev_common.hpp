@@ -1,7 +1,18 @@
 // dev_common.hpp -- small gfx950 device helpers shared by the coding and CRC kernels.
+//
+// Also compiled by hipRTC (rtc.hip: decode networks built per erasure pattern at run time), where
+// no standard headers exist: the fixed-width types come from hipRTC's own runtime header.
 #pragma once
+#ifdef __HIPCC_RTC__
+using uint8_t = __hip_internal::uint8_t;
+using uint32_t = __hip_internal::uint32_t;
+using uint64_t = __hip_internal::uint64_t;
+using int32_t = __hip_internal::int32_t;
+using uintptr_t = unsigned long;
+#else
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#endif
 
 namespace blbrs {
 namespace dev {

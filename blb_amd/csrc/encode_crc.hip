@@ -37,6 +37,7 @@
 #include <set>
 
 #include "crc_device.hpp"
+#include "tuning.hpp"
 #include "gf_device.hpp"
 
 namespace blbrs {
@@ -363,7 +364,7 @@ bool encode_crc_supported(const EncodeCrcArgs& a) { return encode_crc_tile_suppo
 hipError_t launch_encode_crc(const EncodeCrcArgs& in, hipStream_t stream) {
     if (in.B == 0 || in.S == 0) return hipSuccess;
     if (!encode_crc_supported(in) || !in.crc) return hipErrorInvalidValue;
-    const bool persistent = getenv("BLBRS_EC_PERSISTENT") != nullptr;  // per call: A/B in one process
+    const bool persistent = tune::get(tune::kEcPersistent) != 0;  // A/B in one process (tuning.hpp)
     if ((!persistent || !segment_supported(in)) && encode_crc_tile_supported(in))
         return launch_encode_crc_tile(in, stream);
     const KernelFn fn = pick(in.k, in.rows);
@@ -397,7 +398,7 @@ hipError_t launch_encode_crc(const EncodeCrcArgs& in, hipStream_t stream) {
     a.segs_per_block = static_cast<uint32_t>((a.block + kSeg - 1) / kSeg);
     a.total_segs = static_cast<uint64_t>(in.B) * a.nblocks * a.segs_per_block;
     a.c = c;
-    if (const char* f = getenv("BLBRS_EC_FLAGS")) a.flags = static_cast<uint32_t>(atoi(f));
+    if (const long f = tune::get(tune::kEcFlags)) a.flags = static_cast<uint32_t>(f);
     const uint64_t total_blocks = static_cast<uint64_t>(in.rows) * in.B * a.nblocks;
     if (a.total_segs * kWaves > 0x7FFFFFFFull || total_blocks * a.segs_per_block > 0x7FFFFFFFull)
         return hipErrorInvalidValue;

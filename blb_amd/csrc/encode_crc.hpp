@@ -31,7 +31,7 @@ bool encode_crc_supported(const EncodeCrcArgs& a);
 
 // Launches the fused kernel plus the per-block combine on `stream`: the tile-grid kernel
 // (encode_crc_tile.hip) when it covers the shape, else the persistent segment kernel.
-// BLBRS_EC_PERSISTENT=1 forces the segment kernel (A/B measurements).
+// knob BLBRS_EC_PERSISTENT=1 (tuning.hpp) forces the segment kernel (A/B measurements).
 hipError_t launch_encode_crc(const EncodeCrcArgs& a, hipStream_t stream);
 
 // The tile-grid form: k in {3, 4, 6, 8, 10, 12} and rows <= 5, 16-byte aligned base and

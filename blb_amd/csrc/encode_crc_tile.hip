@@ -38,6 +38,7 @@
 #include "crc_device.hpp"
 #include "gf_bitslice.hpp"
 #include "gf_device.hpp"
+#include "tuning.hpp"
 
 namespace blbrs {
 namespace {
@@ -807,7 +808,7 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
     }
 #else
     unsigned occ = 0;  // A/B knob, as rs_kernels.hip: dynamic LDS per workgroup of the network launches
-    if (const char* v = cm ? getenv("BLBRS_OCC_LDS_ECT") : nullptr) occ = static_cast<unsigned>(std::min(atol(v), 65536L));
+    if (const long v = cm ? tune::get(tune::kOccLdsEct) : 0; v > 0) occ = static_cast<unsigned>(std::min(v, 65536L));
     if (groups) hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), occ, stream, a);
 #endif
     e = hipGetLastError();

@@ -17,10 +17,11 @@
 // VALU per 4 bytes of every shard (one dword column): RS(6,3) 81 vs 115 with v_perm tables,
 // RS(10,4) 159 vs 240, RS(12,5) 211 vs 345 (tools/bitslice_count.py).  Decode matrices
 // depend on the erasure pattern and stay on the v_perm path (gf_device.hpp).
+//
+// The same kernels run decode networks too: rtc.hip generates a network for the rows of one
+// erasure pattern at run time and compiles it with hipRTC against these headers, so the device
+// parts below are RTC-clean (no standard headers).
 #pragma once
-#include <cstdint>
-#include <cstdlib>
-
 #include "dev_common.hpp"
 
 namespace blbrs {
@@ -153,6 +154,13 @@ constexpr GroupTerms<K, G> make_group_terms() {
 template <int K, int G>
 constexpr GroupTerms<K, G> kGroupTerms = make_group_terms<K, G>();
 
+#ifndef __HIPCC_RTC__
+}  // namespace bs
+}  // namespace blbrs
+#include "tuning.hpp"
+namespace blbrs {
+namespace bs {
+
 // Host side: true when `rows` (nrows x k, row-major) are parity rows 0..nrows-1 of k, i.e.
 // a pass the compiled network computes.
 template <int K>
@@ -179,11 +187,8 @@ inline bool is_parity_rows(const uint8_t* rows, int nrows, int k) {
 // the table multiply is VALU-bound, k + rows > `wide` (each kernel passes its own measured
 // threshold).  Where the table kernel already runs at the access pattern's speed (RS(6,3)) it
 // folds each input pair as its loads land and stays 2-5 % ahead of the network.
-// BLBRS_BITSLICE, read per launch (A/B runs): 0 = never, 2 = every compiled shape.
-inline int mode() {
-    const char* e = getenv("BLBRS_BITSLICE");
-    return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
-}
+// Knob BLBRS_BITSLICE (tuning.hpp; A/B runs): 0 = never, 2 = every compiled shape.
+inline int mode() { return static_cast<int>(tune::get(tune::kBitslice)); }
 inline bool use(bool parity, int k, int rows, int wide) {
     if (!parity) return false;
     const int m = mode();
@@ -192,6 +197,7 @@ inline bool use(bool parity, int k, int rows, int wide) {
 // Thresholds per kernel: rs_code_kernel (k + rows > 9 is also where it drops to U = 2), the
 // fused encode+CRC tile kernel, PackTracts + Encode.
 constexpr int kWideCode = 9, kWideTile = 11, kWidePack = 9;
+#endif  // __HIPCC_RTC__
 
 // --- device ----------------------------------------------------------------------------
 
@@ -252,6 +258,30 @@ __device__ __forceinline__ void parity_rows(const uint32_t (&x)[K][8], uint32_t 
         parity_rows<K, MR, R + 1>(x, out);
     }
 }
+
+// The network the coding kernel runs (rs_code_kernel's NET parameter): NET::rows<MR>(x, out)
+// takes every input's planes (x, transposed by the caller) and returns rows 0..MR-1 in byte
+// form.  EncodeNet<K> is the encode matrix compiled into the library; rtc.hip generates the
+// same interface for decode rows.
+template <int K>
+struct EncodeNet {
+    template <int MR>
+    __device__ static __forceinline__ void rows(const uint32_t (&x)[K][8], uint32_t (&out)[MR][8]) {
+        parity_rows<K, MR>(x, out);
+    }
+};
+
+// rs_code_kernel's call into its NET (void: the table path, never called).
+template <class NET, int K, int MR>
+struct NetRows {
+    __device__ static __forceinline__ void run(const uint32_t (&x)[K][8], uint32_t (&out)[MR][8]) {
+        NET::template rows<MR>(x, out);
+    }
+};
+template <int K, int MR>
+struct NetRows<void, K, MR> {
+    __device__ static __forceinline__ void run(const uint32_t (&)[K][8], uint32_t (&)[MR][8]) {}
+};
 
 // acc ^ the terms [J, n) of input group GI for parity row R, output bit P (x: every input's
 // planes, those of group GI transposed).  Every index is bound to a constexpr int first:

@@ -11,7 +11,7 @@
 // leaves the source buffer's pages.  Region heads/tails (< 16 bytes) go byte by byte.
 #include "pack.hpp"
 
-#include <cstdlib>
+#include "tuning.hpp"
 
 namespace blbrs {
 namespace {
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
 
 using PackFn = void (*)(PackArgs);
 
-// Variants (A/B knob BLBRS_PACK_VARIANT, read per launch; tools/pack_ab.py,
+// Variants (A/B knob BLBRS_PACK_VARIANT, tuning.hpp; tools/pack_ab.py,
 // profiles/r03/pack/): 6 = the default: XCD map, the whole 64 KiB tile (16 chunks per lane)
 // in flight, cached loads, DPP neighbour block; 0 = the round-2 kernel (two loads per
 // misaligned chunk, 4 chunks per lane, no XCD map); 8 = 6 with nontemporal loads and 8 chunks;
@@ -196,8 +196,8 @@ using PackFn = void (*)(PackArgs);
 #define BLBRS_PACK_DEFAULT 6
 #endif
 PackFn pick_pack(bool& remap) {
-    const char* e = getenv("BLBRS_PACK_VARIANT");
-    const int v = e ? atoi(e) : BLBRS_PACK_DEFAULT;
+    const long knob = tune::get(tune::kPackVariant);  // BLBRS_PACK_VARIANT (tuning.hpp)
+    const int v = knob >= 0 ? static_cast<int>(knob) : BLBRS_PACK_DEFAULT;
     remap = v != 0;
     switch (v) {
         case 0: return pack_kernel<false, false, 4, false>;

@@ -1,7 +1,8 @@
 // rs_kernels.hpp -- launch interface of the GF(2^8) coding kernels (rs_kernels.hip).
+// The struct and constants are also compiled by hipRTC (rtc.hip); the host launch interface
+// is not.
 #pragma once
-#include <hip/hip_runtime.h>
-#include <cstdint>
+#include "dev_common.hpp"
 
 namespace blbrs {
 
@@ -41,12 +42,24 @@ constexpr int kMaxRows = 8;                               // outputs per pass
 // are compared, so every shard is read or written once.
 enum class Mode : int { kStore = 0, kVerify = 1, kStoreVerify = 2 };
 
+// 16-byte chunks per lane per tile of the network kernels (compiled encode networks and run-time
+// decode networks alike): 4 in store mode when k + rows <= 9, else 2.  The network holds fewer
+// registers than the table multiply (no bit groups, no table operands), so verify keeps U = 2 on
+// every shape (RS(12,5): 154 VGPRs).
+constexpr int network_u(int k, int rows, int mode) { return mode == 0 ? (k + rows <= 9 ? 4 : 2) : 2; }
+
+#ifndef __HIPCC_RTC__
+namespace rtc {
+struct NetKernel;
+}
 // Launches one pass over args.B stripes on `stream` (grid, tiles and XCD mapping chosen
-// here); returns hipSuccess or the launch error.
-hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream);
+// here); returns hipSuccess or the launch error.  `net`: the pass's run-time network
+// (rtc.hpp), used when loaded, else the ahead-of-time kernel.
+hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, const rtc::NetKernel* net = nullptr);
 
 // Name of the kernel instantiation launch_code() would pick (for profiling/tests).
 const char* kernel_name(int k, int rows, Mode mode, bool parity = false);
+#endif
 
 
 }  // namespace blbrs

@@ -1,0 +1,414 @@
+// rtc.hip -- decode networks compiled at run time with hipRTC (see rtc.hpp).
+#include "rtc.hpp"
+
+#include <hip/hiprtc.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "gf256.hpp"
+#include "tuning.hpp"
+
+namespace blbrs {
+namespace rtc {
+namespace {
+
+// The device headers rs_code.hpp needs, embedded at build time (Makefile: _build/rtc_headers.inc
+// wraps each file in a raw string), so the library compiles against exactly the source it was
+// built from and needs no file next to it.
+struct Header {
+    const char* name;
+    const char* src;
+};
+const Header kHeaders[] = {
+#include "rtc_headers.inc"
+};
+
+constexpr int kMaxK = 16;      // inputs a run-time network takes (planes: 8 VGPRs per input)
+constexpr int kMaxNetRows = 8;  // = kMaxRows
+constexpr size_t kMaxEntries = 512;  // kernels kept per process; past it, passes stay on tables
+
+// --- network generation --------------------------------------------------------------------
+
+// Output plane (r, p) = XOR of input planes (c, q) with bit p of coef[r][c] * 2^q set
+// (multiplying by a constant is GF(2)-linear).  With `cse`, a pair of signals that appears in
+// three or more outputs becomes one temporary (greedy, most frequent pair first, temporaries may
+// pair again: Paar's heuristic); an output of T signals then costs ceil((T - 1) / 2) v_bitop3
+// XOR3s and a temporary one XOR.  The cheaper of the two forms is emitted.
+struct Net {
+    int nin = 0;
+    std::vector<std::pair<int, int>> temps;  // signal nin + i = first ^ second
+    std::vector<std::vector<int>> outs;      // per output plane, its signals
+
+    int ops() const {
+        int n = static_cast<int>(temps.size());
+        for (const auto& o : outs) n += o.size() <= 1 ? 0 : static_cast<int>(o.size()) / 2;
+        return n;
+    }
+};
+
+Net plain_net(int k, int rows, const uint8_t* coef) {
+    const GF& g = gf();
+    Net net;
+    net.nin = 8 * k;
+    net.outs.resize(static_cast<size_t>(rows) * 8);
+    for (int r = 0; r < rows; ++r)
+        for (int c = 0; c < k; ++c)
+            for (int q = 0; q < 8; ++q) {
+                const uint8_t col = g.mul(coef[r * k + c], static_cast<uint8_t>(1u << q));
+                for (int p = 0; p < 8; ++p)
+                    if ((col >> p) & 1u) net.outs[r * 8 + p].push_back(c * 8 + q);
+            }
+    return net;
+}
+
+void share_pairs(Net& net) {
+    for (;;) {
+        const int nsig = net.nin + static_cast<int>(net.temps.size());
+        std::vector<int> cnt(static_cast<size_t>(nsig) * nsig, 0);
+        for (auto& o : net.outs) {
+            std::sort(o.begin(), o.end());
+            for (size_t i = 0; i < o.size(); ++i)
+                for (size_t j = i + 1; j < o.size(); ++j) ++cnt[static_cast<size_t>(o[i]) * nsig + o[j]];
+        }
+        int best = 0, ba = -1, bb = -1;
+        for (int a = 0; a < nsig; ++a)
+            for (int b = a + 1; b < nsig; ++b)
+                if (cnt[static_cast<size_t>(a) * nsig + b] > best) {
+                    best = cnt[static_cast<size_t>(a) * nsig + b];
+                    ba = a;
+                    bb = b;
+                }
+        if (best < 3) return;
+        const int s = nsig;
+        net.temps.emplace_back(ba, bb);
+        for (auto& o : net.outs) {
+            auto ia = std::find(o.begin(), o.end(), ba), ib = std::find(o.begin(), o.end(), bb);
+            if (ia == o.end() || ib == o.end()) continue;
+            o.erase(std::remove_if(o.begin(), o.end(), [&](int v) { return v == ba || v == bb; }), o.end());
+            o.push_back(s);
+        }
+    }
+}
+
+std::string sig_name(const Net& net, int s) {
+    if (s < net.nin) return "x[" + std::to_string(s / 8) + "][" + std::to_string(s % 8) + "]";
+    return "t" + std::to_string(s - net.nin);
+}
+
+std::string emit(const Net& net, int k, int rows) {
+    std::string o;
+    o += "struct BlbrsNet {\n  template <int MR>\n  __device__ static __forceinline__ void rows(const uint32_t (&x)[" +
+         std::to_string(k) + "][8], uint32_t (&o)[MR][8]) {\n";
+    o += "    static_assert(MR == " + std::to_string(rows) + ", \"rows\");\n";
+    o += "    using blbrs::dev::xor3;\n";
+    for (size_t i = 0; i < net.temps.size(); ++i)
+        o += "    const uint32_t t" + std::to_string(i) + " = " + sig_name(net, net.temps[i].first) + " ^ " +
+             sig_name(net, net.temps[i].second) + ";\n";
+    for (int r = 0; r < rows; ++r)
+        for (int p = 0; p < 8; ++p) {
+            const auto& s = net.outs[r * 8 + p];
+            std::string e;
+            if (s.empty()) {
+                e = "0u";
+            } else if (s.size() == 1) {
+                e = sig_name(net, s[0]);
+            } else if (s.size() == 2) {
+                e = sig_name(net, s[0]) + " ^ " + sig_name(net, s[1]);
+            } else {
+                e = "xor3(" + sig_name(net, s[0]) + ", " + sig_name(net, s[1]) + ", " + sig_name(net, s[2]) + ")";
+                size_t i = 3;
+                for (; i + 1 < s.size(); i += 2) e = "xor3(" + e + ", " + sig_name(net, s[i]) + ", " + sig_name(net, s[i + 1]) + ")";
+                if (i < s.size()) e = "(" + e + " ^ " + sig_name(net, s[i]) + ")";
+            }
+            o += "    o[" + std::to_string(r) + "][" + std::to_string(p) + "] = " + e + ";\n";
+        }
+    o += "#pragma unroll\n    for (int r = 0; r < MR; ++r) blbrs::bs::transpose8(o[r]);\n  }\n};\n";
+    return o;
+}
+
+// --- state ---------------------------------------------------------------------------------
+
+struct Compiled {
+    std::vector<char> code;
+    std::string lowered;
+};
+
+struct Job {
+    std::string src, name_expr;
+    int device = 0;
+    NetKernel* nk = nullptr;
+};
+
+struct State {
+    std::mutex mu;
+    std::condition_variable cv_idle;
+    std::map<std::string, std::unique_ptr<NetKernel>> kernels;        // device|source
+    std::map<std::string, std::shared_ptr<Compiled>> compiled;        // source
+    std::deque<Job> queue;
+    bool worker = false;
+    int busy = 0;
+    bool exiting = false;
+    Stats st;
+    std::string first_failure;
+};
+State& S() {
+    static State* s = new State;  // never destroyed: a worker may outlive static destructors
+    return *s;
+}
+
+void note_failure(State& s, const std::string& what) {
+    ++s.st.failed;
+    if (s.first_failure.empty()) {
+        s.first_failure = what;
+        std::fprintf(stderr, "blbrs: run-time decode network unavailable, tables used instead: %.400s\n", what.c_str());
+    }
+}
+
+// Compile (outside the lock); nullptr + log on failure.
+std::shared_ptr<Compiled> compile(const std::string& src, const std::string& name_expr, std::string* log) {
+    std::vector<const char*> names, srcs;
+    for (const Header& h : kHeaders) {
+        names.push_back(h.name);
+        srcs.push_back(h.src);
+    }
+    hiprtcProgram prog = nullptr;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "blbrs_net.hip", static_cast<int>(names.size()), srcs.data(),
+                            names.data()) != HIPRTC_SUCCESS) {
+        *log = "hiprtcCreateProgram failed";
+        return nullptr;
+    }
+    hiprtcAddNameExpression(prog, name_expr.c_str());
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    std::shared_ptr<Compiled> out;
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string l(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &l[0]);
+        *log = std::string(hiprtcGetErrorString(rc)) + ": " + l;
+    } else {
+        out = std::make_shared<Compiled>();
+        size_t n = 0;
+        hiprtcGetCodeSize(prog, &n);
+        out->code.resize(n);
+        hiprtcGetCode(prog, out->code.data());
+        const char* lowered = nullptr;
+        if (hiprtcGetLoweredName(prog, name_expr.c_str(), &lowered) != HIPRTC_SUCCESS || !lowered) {
+            *log = "hiprtcGetLoweredName failed for " + name_expr;
+            out.reset();
+        } else {
+            out->lowered = lowered;
+        }
+    }
+    hiprtcDestroyProgram(&prog);
+    return out;
+}
+
+// Compile if needed, then load on job.device (made current here) and publish the function.
+void run_job(State& s, const Job& j) {
+    std::shared_ptr<Compiled> c;
+    {
+        std::lock_guard<std::mutex> g(s.mu);
+        auto it = s.compiled.find(j.src);
+        if (it != s.compiled.end()) c = it->second;
+    }
+    if (!c) {
+        std::string log;
+        const auto t0 = std::chrono::steady_clock::now();
+        c = compile(j.src, j.name_expr, &log);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::lock_guard<std::mutex> g(s.mu);
+        s.st.compile_ms += ms;
+        if (!c) {
+            note_failure(s, log);
+            j.nk->state.store(-1);
+            return;
+        }
+        ++s.st.compiled;
+        s.compiled[j.src] = c;
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    hipError_t e = hipSetDevice(j.device);
+    if (e == hipSuccess) e = hipModuleLoadData(&mod, c->code.data());
+    if (e == hipSuccess) e = hipModuleGetFunction(&fn, mod, c->lowered.c_str());
+    (void)hipSetDevice(prev);
+    std::lock_guard<std::mutex> g(s.mu);
+    if (e != hipSuccess || !fn) {
+        (void)hipGetLastError();
+        note_failure(s, std::string("module load: ") + hipGetErrorString(e));
+        j.nk->state.store(-1);
+        return;
+    }
+    ++s.st.loaded;
+    j.nk->fn.store(fn);
+    j.nk->state.store(1);
+}
+
+void worker_loop() {
+    State& s = S();
+    std::unique_lock<std::mutex> lk(s.mu);
+    while (!s.queue.empty() && !s.exiting) {
+        Job j = std::move(s.queue.front());
+        s.queue.pop_front();
+        ++s.busy;
+        lk.unlock();
+        run_job(s, j);
+        lk.lock();
+        --s.busy;
+        if (s.st.pending) --s.st.pending;
+    }
+    s.worker = false;
+    s.cv_idle.notify_all();
+}
+
+// At exit: stop taking jobs and let a running compile finish before HIP tears down (this handler
+// is registered after HIP initialised, so it runs first).
+void at_exit() {
+    State& s = S();
+    std::unique_lock<std::mutex> lk(s.mu);
+    s.exiting = true;
+    s.st.pending -= std::min<uint64_t>(s.st.pending, s.queue.size());
+    s.queue.clear();
+    s.cv_idle.wait_for(lk, std::chrono::seconds(60), [&] { return !s.worker; });
+}
+
+std::string kernel_source(int k, int rows, const uint8_t* coef, bool cse, int* ops) {
+    Net plain = plain_net(k, rows, coef);
+    Net net = plain;
+    if (cse) {
+        share_pairs(net);
+        if (net.ops() >= plain.ops()) net = plain;
+    }
+    if (ops) *ops = net.ops();
+    return emit(net, k, rows);
+}
+
+}  // namespace
+
+// Single-row passes (the client's usual ReconstructData) stay on tables: the network transposes
+// all k inputs for one output row and measured 0.2-1 % slower there (profiles/r04/rpc_shapes).
+bool eligible(int k, int rows) {
+    const long mode = tune::get(tune::kRtc);
+    return mode != 0 && k >= 2 && k <= kMaxK && rows >= 2 && rows <= kMaxNetRows &&
+           k + rows > tune::get(tune::kRtcWide);
+}
+
+std::string network_source(int k, int rows, const uint8_t* coef, bool cse, int* ops) {
+    return kernel_source(k, rows, coef, cse, ops);
+}
+
+namespace {
+// The translation unit hipRTC compiles for one pass, and the kernel's name expression.
+void unit(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::string* src, std::string* name, int* u,
+          int* ops) {
+    const int imode = static_cast<int>(mode), addr = strided ? 0 : 1;
+    *u = network_u(k, rows, imode);
+    *src = "#include \"rs_code.hpp\"\n" + kernel_source(k, rows, coef, tune::get(tune::kRtcCse) != 0, ops);
+    *name = "blbrs::code::rs_code_kernel<" + std::to_string(k) + ", " + std::to_string(rows) + ", " +
+            std::to_string(imode) + ", " + std::to_string(addr) + ", " + std::to_string(*u) + ", 3, BlbrsNet>";
+    *src += "// " + *name + "\n";
+}
+}  // namespace
+
+bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::string* log) {
+    std::string src, name;
+    int u = 0, ops = 0;
+    unit(k, rows, mode, strided, coef, &src, &name, &u, &ops);
+    State& s = S();
+    {
+        std::lock_guard<std::mutex> g(s.mu);
+        if (s.compiled.count(src)) return true;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    auto c = compile(src, name, log);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    std::lock_guard<std::mutex> g(s.mu);
+    s.st.compile_ms += ms;
+    if (!c) return false;
+    ++s.st.compiled;
+    s.compiled[src] = c;
+    return true;
+}
+
+NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const uint8_t* coef) {
+    if (!eligible(k, rows)) return nullptr;
+    std::string src, name;
+    int u = 0, ops = 0;
+    unit(k, rows, mode, strided, coef, &src, &name, &u, &ops);
+    const std::string key = std::to_string(device) + "|" + src;
+    State& s = S();
+    NetKernel* nk = nullptr;
+    bool sync = false;
+    {
+        std::lock_guard<std::mutex> g(s.mu);
+        auto it = s.kernels.find(key);
+        if (it != s.kernels.end()) return it->second.get();
+        if (s.exiting || s.kernels.size() >= kMaxEntries) return nullptr;
+        auto p = std::make_unique<NetKernel>();
+        p->u = u;
+        p->ops = ops;
+        nk = p.get();
+        s.kernels.emplace(key, std::move(p));
+        ++s.st.requested;
+        sync = tune::get(tune::kRtc) == 2;
+        if (!sync) {
+            s.queue.push_back(Job{src, name, device, nk});
+            ++s.st.pending;
+            if (!s.worker) {
+                static std::once_flag once;
+                std::call_once(once, [] { std::atexit(at_exit); });
+                s.worker = true;
+                std::thread(worker_loop).detach();
+            }
+        } else {
+            ++s.busy;
+        }
+    }
+    if (sync) {
+        run_job(s, Job{src, name, device, nk});
+        std::lock_guard<std::mutex> g(s.mu);
+        --s.busy;
+        s.cv_idle.notify_all();
+    }
+    return nk;
+}
+
+Stats stats() {
+    State& s = S();
+    std::lock_guard<std::mutex> g(s.mu);
+    return s.st;
+}
+
+bool wait_idle(long timeout_ms) {
+    State& s = S();
+    std::unique_lock<std::mutex> lk(s.mu);
+    auto idle = [&] { return s.queue.empty() && !s.worker && s.busy == 0; };
+    if (timeout_ms < 0) {
+        s.cv_idle.wait(lk, idle);
+        return true;
+    }
+    return s.cv_idle.wait_for(lk, std::chrono::milliseconds(timeout_ms), idle);
+}
+
+std::string first_failure() {
+    State& s = S();
+    std::lock_guard<std::mutex> g(s.mu);
+    return s.first_failure;
+}
+
+}  // namespace rtc
+}  // namespace blbrs

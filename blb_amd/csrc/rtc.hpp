@@ -1,0 +1,71 @@
+// rtc.hpp -- decode networks compiled at run time (hipRTC), one per erasure pattern.
+//
+// Encode's coefficients are fixed, so its bit-plane XOR networks are compiled into the library
+// (gf_bitslice.hpp).  A decode pass's rows -- inv(M[valid]) for missing data,
+// P * inv(M[valid]) for missing parity -- depend on which shards are present, i.e. on the
+// erasure pattern of the call (klauspost reedsolomon.go reconstruct; blb's recovery RPC
+// rebuilds every absent slot, internal/tractserver/store.go:1062-1102).  On wide shapes the
+// v_perm table multiply is VALU-bound there too, so for such a pass this module generates the
+// pass's network as straight-line code (XOR terms shared between output planes where that saves
+// instructions), compiles rs_code_kernel<K, MR, MODE, ADDR, U, NT, Net> (rs_code.hpp) with hipRTC
+// against the library's own device headers, and loads it on the device.  The device plan caches
+// the kernel next to the pass's tables -- the counterpart of klauspost's inversion tree, one
+// level further: a compiled kernel per cached inverse.
+//
+// Compilation runs on a background thread by default (knob BLBRS_RTC = 1): the pass keeps the
+// table kernel until its network is loaded, so no call waits on the compiler.  BLBRS_RTC = 2
+// compiles in the calling thread on first use, 0 disables run-time networks.  A compile or
+// load failure leaves the pass on tables (counted in blbrs_rtc_get_stats).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <string>
+
+#include "rs_kernels.hpp"
+
+namespace blbrs {
+namespace rtc {
+
+struct NetKernel {
+    std::atomic<hipFunction_t> fn{nullptr};  // set once loaded
+    std::atomic<int> state{0};               // 0 pending, 1 ready, -1 failed
+    int u = 0;                               // 16-byte chunks per lane per tile
+    int ops = 0;                             // VALU ops of the generated network per 8-dword group
+};
+
+// Per-pass lookup cache (mode x addressing), kept in the device plan.
+struct NetSlot {
+    std::atomic<NetKernel*> k[3][2] = {};
+};
+
+// Whether a pass of `rows` rows over `k` inputs may take a run-time network (the knob
+// BLBRS_RTC is on, rows >= 2 and k + rows > BLBRS_RTC_WIDE); cheap, called per launch.
+bool eligible(int k, int rows);
+
+// The network kernel for (device, rows x k coefficients, mode, addressing), requesting its
+// compilation on first use.  Returns nullptr when not eligible; otherwise an entry that stays
+// valid for the life of the process (fn == nullptr until it is ready).
+NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const uint8_t* coef);
+
+// The generated network's source for rows x k coefficients (tests, tools).
+std::string network_source(int k, int rows, const uint8_t* coef, bool cse, int* ops);
+
+// Compiles the kernel request() would build, without loading it (no device needed); true on
+// success, else false with the compiler log.  Adds to the compile cache.
+bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::string* log);
+
+struct Stats {
+    uint64_t requested = 0, compiled = 0, loaded = 0, failed = 0, pending = 0;
+    double compile_ms = 0;  // total compile time
+};
+Stats stats();
+// Blocks until no compile or load is queued or running, or timeout_ms passes (< 0: forever);
+// true when idle.
+bool wait_idle(long timeout_ms);
+// The compiler log of the first failure ("" if none).
+std::string first_failure();
+
+}  // namespace rtc
+}  // namespace blbrs

@@ -1,8 +1,16 @@
 // runtime.hip -- host runtime of libblbrs (see runtime.hpp).
 #include "runtime.hpp"
 
+#include "tuning.hpp"
+
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cctype>
+#include <cstdio>
 #include <cstdlib>
+#include <shared_mutex>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -155,25 +163,114 @@ std::vector<std::pair<int, int>> lane_keys(const std::vector<int>& devs) {
     return keys;
 }
 
-size_t pick_lane(const std::vector<int>& lanes, std::atomic<unsigned>& rr) {
+size_t pick_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t start, int node) {
+    size_t best = start, best_local = n;
+    for (size_t j = 0; j < n; ++j) {
+        const size_t i = (start + j) % n;
+        if (loads[i] < loads[best]) best = i;
+        if (node >= 0 && nodes[i] == node && (best_local == n || loads[i] < loads[best_local])) best_local = i;
+    }
+    if (best_local < n && loads[best_local] <= loads[best] + kNumaSlackBytes) return best_local;
+    return best;
+}
+
+size_t pick_lane(const std::vector<int>& lanes, std::atomic<unsigned>& rr, int node) {
     const size_t n = lanes.size();
     const auto keys = lane_keys(lanes);
-    auto in_bytes = [&](size_t i) {
+    std::vector<int64_t> loads(n);
+    std::vector<int> nodes(n, -1);
+    for (size_t i = 0; i < n; ++i) {
         const LaneLoad* l = lane_of(keys[i].first, keys[i].second);
-        return l ? l->in_bytes.load(std::memory_order_relaxed) : 0;
-    };
-    const size_t start = rr.fetch_add(1, std::memory_order_relaxed) % n;
-    size_t best = start;
-    int64_t best_load = in_bytes(start);
-    for (size_t j = 1; j < n && best_load > 0; ++j) {
-        const size_t i = (start + j) % n;
-        const int64_t l = in_bytes(i);
-        if (l < best_load) {
-            best = i;
-            best_load = l;
-        }
+        loads[i] = l ? l->in_bytes.load(std::memory_order_relaxed) : 0;
+        if (node >= 0) nodes[i] = device_numa_node(keys[i].first);
     }
-    return best;
+    return pick_lane_policy(nodes.data(), loads.data(), n, rr.fetch_add(1, std::memory_order_relaxed) % n, node);
+}
+
+namespace {
+
+// Device -> NUMA node, -2 = not looked up yet.
+std::atomic<int> g_dev_node[kMaxDevices];
+std::once_flag g_dev_node_once;
+
+int read_device_node(int dev) {
+    char bdf[64] = {};
+    if (hipDeviceGetPCIBusId(bdf, sizeof bdf, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    std::string path = "/sys/bus/pci/devices/";
+    for (const char* c = bdf; *c; ++c) path += static_cast<char>(std::tolower(static_cast<unsigned char>(*c)));
+    path += "/numa_node";
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) return -1;
+    int node = -1;
+    if (std::fscanf(f, "%d", &node) != 1) node = -1;
+    std::fclose(f);
+    return node;
+}
+
+// The node of the page at p (get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR)), -1 if unknown.
+int page_node(const void* p) {
+    int node = -1;
+    constexpr unsigned long kMpolFNode = 1, kMpolFAddr = 2;
+    if (syscall(SYS_get_mempolicy, &node, nullptr, 0ul, p, kMpolFNode | kMpolFAddr) != 0) return -1;
+    return node;
+}
+
+// Pool-handed and registered host buffers -> their node (recorded once per buffer).
+struct NodeMap {
+    std::shared_mutex mu;
+    std::map<uintptr_t, std::pair<size_t, int>> ranges;  // base -> (length, node)
+};
+NodeMap& node_map() {
+    static NodeMap* m = new NodeMap();
+    return *m;
+}
+void note_range(const void* p, size_t n) {
+    const int node = page_node(p);
+    NodeMap& m = node_map();
+    std::unique_lock<std::shared_mutex> g(m.mu);
+    m.ranges[reinterpret_cast<uintptr_t>(p)] = {n, node};
+}
+void drop_range(const void* p) {
+    NodeMap& m = node_map();
+    std::unique_lock<std::shared_mutex> g(m.mu);
+    m.ranges.erase(reinterpret_cast<uintptr_t>(p));
+}
+
+}  // namespace
+
+int device_numa_node(int dev) {
+    if (dev < 0 || dev >= kMaxDevices) return -1;
+    std::call_once(g_dev_node_once, [] {
+        for (auto& v : g_dev_node) v.store(-2);
+    });
+    int v = g_dev_node[dev].load(std::memory_order_acquire);
+    if (v == -2) {
+        v = read_device_node(dev);
+        int expect = -2;
+        if (!g_dev_node[dev].compare_exchange_strong(expect, v)) v = expect;
+    }
+    return v;
+}
+
+int set_device_numa_node(int dev, int node) {
+    if (dev < 0 || dev >= kMaxDevices || node < -1) return fail(BLBRS_ERR_INVALID_ARG, "bad device or node");
+    (void)device_numa_node(dev);  // initialise the table
+    g_dev_node[dev].store(node, std::memory_order_release);
+    return BLBRS_OK;
+}
+
+int host_numa_node(const void* p) {
+    if (!p) return -1;
+    NodeMap& m = node_map();
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::shared_lock<std::shared_mutex> g(m.mu);
+    auto it = m.ranges.upper_bound(a);
+    if (it == m.ranges.begin()) return -1;
+    --it;
+    return a < it->first + it->second.first ? it->second.second : -1;
 }
 
 void LoadTicket::take(int d, int o, uint64_t b) {
@@ -209,7 +306,7 @@ int lane_stats(int dev, int occ, blbrs_lane_stats* out) {
 }
 
 bool zero_copy_policy(int dev, int written, int touched) {
-    if (const char* env = std::getenv("BLBRS_HOST_ZC"); env && *env) return env[0] != '0';
+    if (const long zc = tune::get(tune::kHostZc); zc >= 0) return zc != 0;  // BLBRS_HOST_ZC (tuning.hpp)
     return 4 * written >= touched || load_of(dev) <= kZeroCopyMaxCalls;
 }
 
@@ -619,6 +716,7 @@ int pool_get(size_t n, uint8_t** out, size_t* cap, bool internal) {
     p.live[b] = want;
     *out = b;
     *cap = want;
+    note_range(b, want);  // its NUMA node, for the lane pick (pick_lane)
     return BLBRS_OK;
 }
 
@@ -643,7 +741,10 @@ int pool_put(uint8_t* b) {
             ++p.frees;
         }
     }
-    if (free_it) BLBRS_HIP_TRY(hipHostFree(b));
+    if (free_it) {
+        drop_range(b);
+        BLBRS_HIP_TRY(hipHostFree(b));
+    }
     return BLBRS_OK;
 }
 
@@ -670,6 +771,7 @@ int pool_register(void* ptr, size_t n) {
         return rc != BLBRS_OK ? rc : hip_fail(e, "hipHostRegister");
     }
     ++p.registrations;
+    note_range(ptr, n);  // its NUMA node, for the lane pick (pick_lane)
     return BLBRS_OK;
 }
 
@@ -686,6 +788,7 @@ int pool_unregister(void* ptr) {
         p.registered.erase(it);
         p.registered_bytes -= n;
     }
+    drop_range(ptr);
     BLBRS_HIP_TRY(hipHostUnregister(ptr));
     return BLBRS_OK;
 }
@@ -735,7 +838,10 @@ void pool_trim() {
         p.idle_bytes = 0;
         p.frees += drop.size();
     }
-    for (uint8_t* b : drop) (void)hipHostFree(b);
+    for (uint8_t* b : drop) {
+        drop_range(b);
+        (void)hipHostFree(b);
+    }
 }
 
 }  // namespace rt

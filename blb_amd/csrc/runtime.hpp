@@ -76,8 +76,23 @@ int64_t load_of(int dev);
 // (dev, occ) of every entry of a device list.
 std::vector<std::pair<int, int>> lane_keys(const std::vector<int>& devs);
 // Index into `lanes` of the entry with the fewest BYTES in flight (a 4 KiB degraded read and
-// an 8 MiB increment do not weigh the same); ties rotate through `rr`.
-size_t pick_lane(const std::vector<int>& lanes, std::atomic<unsigned>& rr);
+// an 8 MiB increment do not weigh the same); ties rotate through `rr`.  With `node` >= 0 (the
+// NUMA node holding the call's host shards) the lanes of GPUs attached to that node are
+// preferred: the least-loaded local lane wins unless it carries more than kNumaSlackBytes
+// beyond the least-loaded lane overall (then the host link is the smaller cost than the wait).
+constexpr int64_t kNumaSlackBytes = int64_t{64} << 20;
+size_t pick_lane(const std::vector<int>& lanes, std::atomic<unsigned>& rr, int node = -1);
+// The policy itself, over explicit lane nodes and loads, starting the scan at `start` (tests).
+size_t pick_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t start, int node);
+
+// NUMA topology.  device_numa_node: the node the GPU's PCIe root sits on
+// (/sys/bus/pci/devices/<bdf>/numa_node), cached; -1 when unknown; set_device_numa_node
+// overrides it (containers without sysfs, tests).  host_numa_node: the node of the page at p
+// for memory the pool handed out or registered (recorded once per buffer, with
+// get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR) on its first page), -1 for anything else.
+int device_numa_node(int dev);
+int set_device_numa_node(int dev, int node);
+int host_numa_node(const void* p);
 int lane_stats(int dev, int occ, blbrs_lane_stats* out);
 
 // Holds one call's load on a lane (and its device) for the call's duration.
@@ -94,7 +109,7 @@ struct LoadTicket {
 // (Encode: the kernel's posted writes run beside its reads), and for read-dominated calls
 // (ReconstructData: k in, 1 out) while at most kZeroCopyMaxCalls host calls are in flight on
 // the device (this one included); beyond that the copy engines move the inputs faster.
-// $BLBRS_HOST_ZC = 1 / 0 (read per call) forces either way for A/B runs.
+// knob BLBRS_HOST_ZC = 1 / 0 (tuning.hpp) forces either way for A/B runs.
 constexpr int64_t kZeroCopyMaxCalls = 3;
 bool zero_copy_policy(int dev, int written, int touched);
 

@@ -65,3 +65,53 @@ def aggregate_gibps(bytes_per_rank: float, seconds_per_rank: float, device=None)
     total = sum_over_ranks(bytes_per_rank, device)
     t = max_over_ranks(seconds_per_rank, device)
     return total / float(1 << 30) / t
+
+
+# ---- NUMA placement of a rank (one process per GPU on a 2-socket, 8-GPU host) ----
+
+_SYS_SET_MEMPOLICY = 238   # x86_64
+_MPOL_PREFERRED = 1
+
+
+def parse_cpulist(text: str) -> set:
+    """ "0-3,8,10-11" -> {0, 1, 2, 3, 8, 10, 11} (sysfs cpulist format)."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            lo, hi = part.split("-")
+            cpus.update(range(int(lo), int(hi) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+def bind_to_node(node: int, sysfs: str = "/sys/devices/system/node") -> dict:
+    """Bind this process's CPUs to `node`'s (intersected with the affinity it already has, so a
+    job's cgroup share is respected) and make `node` the preferred node for its future page
+    allocations (set_mempolicy MPOL_PREFERRED: pinned host stripes land next to the GPU and fall
+    back to other nodes only when it is full).  Call before any pin_memory.  Returns what was
+    done; nothing is changed when the node is unknown or the intersection is empty."""
+    import ctypes
+    out = {"node": node, "cpus_bound": 0, "mempolicy": None, "bound": False}
+    if node is None or node < 0:
+        out["reason"] = "GPU NUMA node unknown"
+        return out
+    try:
+        cpus = parse_cpulist(open(os.path.join(sysfs, f"node{node}", "cpulist")).read())
+    except OSError as e:
+        out["reason"] = f"no cpulist: {e}"
+        return out
+    mine = os.sched_getaffinity(0)
+    both = cpus & mine
+    if both:
+        os.sched_setaffinity(0, both)
+        out["cpus_bound"] = len(both)
+    else:
+        out["reason"] = "node's CPUs outside this job's affinity"
+    mask = ctypes.c_ulong(1 << node) if node < 64 else None
+    if mask is not None:
+        libc = ctypes.CDLL(None, use_errno=True)
+        rc = libc.syscall(_SYS_SET_MEMPOLICY, _MPOL_PREFERRED, ctypes.byref(mask), ctypes.c_ulong(64))
+        out["mempolicy"] = "preferred" if rc == 0 else f"failed errno {ctypes.get_errno()}"
+    out["bound"] = bool(both) and out["mempolicy"] == "preferred"
+    return out

@@ -165,10 +165,13 @@ class Encoder:
         _check(self._lib.blbrs_matrix(self._h, out.ctypes.data, out.size))
         return out
 
-    def compiled_network(self) -> bool:
-        """True when Encode / Verify run the compiled bit-plane network for this (k, m)
-        (blbrs_encoder_compiled_network); False on the v_perm table path."""
-        return bool(self._lib.blbrs_encoder_compiled_network(self._h))
+    def compiled_network(self) -> dict:
+        """Which kernels run this encoder's Encode as a bit-plane XOR network rather than the
+        v_perm tables (blbrs_encoder_compiled_network): code (rs_code_kernel: Encode / Verify),
+        tile (fused encode+CRC), pack (PackTracts + Encode), rtc (a network compiled at run
+        time for k outside the library's compiled list)."""
+        bits = int(self._lib.blbrs_encoder_compiled_network(self._h))
+        return {"code": bool(bits & 1), "tile": bool(bits & 2), "pack": bool(bits & 4), "rtc": bool(bits & 8)}
 
     # ---- helpers ----
     def _arrays(self, shards, n):
@@ -564,6 +567,125 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     _check(_lib.load().blbrs_device_count(ctypes.byref(n)))
     return n.value
+
+
+# ---- NUMA placement (include/blb_rs.h) ----
+
+def device_numa_node(device: int) -> int:
+    n = ctypes.c_int(-1)
+    _check(_lib.load().blbrs_device_numa_node(int(device), ctypes.byref(n)))
+    return int(n.value)
+
+
+def set_device_numa_node(device: int, node: int) -> None:
+    _check(_lib.load().blbrs_set_device_numa_node(int(device), int(node)))
+
+
+def host_numa_node(buf) -> int:
+    """Node recorded for the pool / registered buffer holding `buf` (numpy array or address)."""
+    addr = buf if isinstance(buf, int) else buf.__array_interface__["data"][0]
+    n = ctypes.c_int(-1)
+    _check(_lib.load().blbrs_host_numa_node(ctypes.c_void_p(addr), ctypes.byref(n)))
+    return int(n.value)
+
+
+def lane_policy(nodes: Sequence[int], loads: Sequence[int], start: int, node: int) -> int:
+    """The library's lane pick (runtime pick_lane_policy) over explicit lanes."""
+    n = len(nodes)
+    na = (ctypes.c_int * n)(*nodes)
+    la = (ctypes.c_int64 * n)(*loads)
+    out = ctypes.c_size_t(0)
+    _check(_lib.load().blbrs_lane_policy(na, la, n, int(start), int(node), ctypes.byref(out)))
+    return int(out.value)
+
+
+# ---- A/B knobs and run-time decode networks (include/blb_rs.h) ----
+
+def set_tuning(name: str, value: int) -> None:
+    """Set a library knob (BLBRS_BITSLICE, BLBRS_RTC, ...; read from the environment once, at
+    load, and changed only through this call)."""
+    _check(_lib.load().blbrs_set_tuning(name.encode(), int(value)))
+
+
+def get_tuning(name: str) -> int:
+    v = ctypes.c_long(0)
+    _check(_lib.load().blbrs_get_tuning(name.encode(), ctypes.byref(v)))
+    return int(v.value)
+
+
+class tuning:
+    """Context manager: `with rs.tuning(BLBRS_BITSLICE=0): ...` sets knobs and restores them."""
+
+    def __init__(self, **knobs):
+        self._knobs = knobs
+        self._old = {}
+
+    def __enter__(self):
+        for k, v in self._knobs.items():
+            self._old[k] = get_tuning(k)
+            set_tuning(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self._old.items():
+            set_tuning(k, v)
+        return False
+
+
+_KNOB_START = {}
+
+
+def use_knobs(env: dict) -> None:
+    """A/B drivers: set exactly the knobs in `env` (BLBRS_* name -> value) and put every knob an
+    earlier call set, and `env` does not name, back to its starting value."""
+    for name in list(_KNOB_START):
+        if name not in env:
+            set_tuning(name, _KNOB_START[name])
+    for name, value in env.items():
+        if name not in _KNOB_START:
+            _KNOB_START[name] = get_tuning(name)
+        set_tuning(name, int(value))
+
+
+def rtc_stats() -> dict:
+    st = _lib.RtcStats()
+    _check(_lib.load().blbrs_rtc_get_stats(ctypes.byref(st)))
+    return {f: (float(getattr(st, f)) if f == "compile_ms" else int(getattr(st, f))) for f, _ in st._fields_}
+
+
+def rtc_wait(timeout_ms: int = -1) -> bool:
+    """Wait for queued run-time networks to compile and load; False on timeout."""
+    rc = _lib.load().blbrs_rtc_wait(int(timeout_ms))
+    if rc == ErrLimit.code:
+        return False
+    _check(rc)
+    return True
+
+
+def rtc_eligible(k: int, rows: int) -> bool:
+    """Whether a decode pass of `rows` rows over k inputs takes a run-time network under the
+    current knobs (rtc.hpp eligible(): BLBRS_RTC on, rows >= 2, k + rows > BLBRS_RTC_WIDE)."""
+    return (get_tuning("BLBRS_RTC") != 0 and get_tuning("BLBRS_BITSLICE") != 0 and 2 <= k <= 16
+            and 2 <= rows <= 8 and k + rows > get_tuning("BLBRS_RTC_WIDE"))
+
+
+def rtc_network_source(coef: np.ndarray, cse: bool = True) -> tuple[str, int]:
+    """(device source, VALU ops per 8-dword group) of the network for a rows x k coefficient
+    matrix."""
+    c = np.ascontiguousarray(coef, dtype=np.uint8)
+    rows, k = c.shape
+    buf = ctypes.create_string_buffer(1 << 20)
+    ops = ctypes.c_int(0)
+    _check(_lib.load().blbrs_rtc_network_source(k, rows, c.ctypes.data, int(cse), buf, len(buf), ctypes.byref(ops)))
+    return buf.value.decode(), int(ops.value)
+
+
+def rtc_compile(coef: np.ndarray, mode: int = 0, strided: bool = True) -> None:
+    """Compile (no device needed) the network kernel of a rows x k coefficient matrix; raises
+    ErrHIP with the compiler log on failure."""
+    c = np.ascontiguousarray(coef, dtype=np.uint8)
+    rows, k = c.shape
+    _check(_lib.load().blbrs_rtc_compile(k, rows, c.ctypes.data, int(mode), int(strided)))
 
 
 def version() -> str:

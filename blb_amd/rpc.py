@@ -27,6 +27,7 @@ keeps blb's pool as it is and pins the buffers the pool creates instead:
 from __future__ import annotations
 
 import threading
+import time
 import weakref
 
 import numpy as np
@@ -43,7 +44,8 @@ _PAGE = 4096
 _mu = threading.RLock()
 _free: dict[int, list] = {c: [] for c in CLASSES}   # sync.Pool contents per class
 _pinned: set[int] = set()                           # base addresses currently registered
-stats = {"registered": 0, "refused": 0, "unregistered": 0, "reregistered": 0}
+stats = {"registered": 0, "refused": 0, "unregistered": 0, "reregistered": 0,
+         "register_s": 0.0, "unregister_s": 0.0}   # wall time inside blbrs_buffer_(un)register
 
 
 def _unregister(addr: int) -> None:
@@ -52,18 +54,25 @@ def _unregister(addr: int) -> None:
             return
         _pinned.discard(addr)
         stats["unregistered"] += 1
+    t0 = time.perf_counter()
     _lib.load().blbrs_buffer_unregister(addr)
+    with _mu:
+        stats["unregister_s"] += time.perf_counter() - t0
 
 
 def _register(base: np.ndarray) -> bool:
     addr = base.ctypes.data
-    if _lib.load().blbrs_buffer_register(addr, base.size) != 0:
+    t0 = time.perf_counter()
+    rc = _lib.load().blbrs_buffer_register(addr, base.size)
+    dt = time.perf_counter() - t0
+    if rc != 0:
         with _mu:
             stats["refused"] += 1
         return False
     with _mu:
         _pinned.add(addr)
         stats["registered"] += 1
+        stats["register_s"] += dt
     return True
 
 

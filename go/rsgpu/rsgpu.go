@@ -301,9 +301,10 @@ func (e *encoder) cpuEncoder() (reedsolomon.Encoder, error) {
 }
 
 // marshal builds C arrays of shard pointers and lengths.  cgo forbids storing Go pointers
-// in C memory unless they are pinned, so every non-empty shard is pinned for the call
-// (Pin does nothing for pool buffers, which are C memory); the C side does not retain any
-// pointer after returning.  A missing shard that has capacity (klauspost reslices
+// in C memory unless they are pinned, so every non-empty shard is pinned with runtime.Pinner
+// for the call -- pool buffers included: they are Go-heap memory (GetBuffer below), and their
+// HIP registration (page-locked for DMA) is a different thing from cgo's pinning rule.  The
+// C side does not retain any pointer after returning.  A missing shard that has capacity (klauspost reslices
 // shards[i][0:size] when cap >= size; client/blb/reconstruct.go:172 relies on it) passes its
 // backing array as the output buffer.
 type marshalled struct {

@@ -127,11 +127,20 @@ int blbrs_data_shards(const blbrs_encoder* enc);
 int blbrs_parity_shards(const blbrs_encoder* enc);
 /* Copies the (k+m)*k encoding matrix (row-major) into out; cap must be >= (k+m)*k. */
 int blbrs_matrix(const blbrs_encoder* enc, uint8_t* out, size_t cap);
-/* 1 when this encoder's Encode / Verify passes run the compiled bit-plane network (the
- * parity rows of (k, m) built into the library, gf_bitslice.hpp: k in {3,4,6,8,10,12},
- * m <= 5; by default only where it is faster, k + m > 9; BLBRS_BITSLICE=0 never, =2 every
- * compiled shape), 0 when they run the v_perm table path.  Same bytes either way; a
+/* Which kernels run this encoder's Encode as a bit-plane XOR network instead of the v_perm
+ * table multiply, one bit per kernel (each kernel has its own measured threshold):
+ *   BLBRS_NET_CODE  rs_code_kernel (Encode / Verify): the parity rows compiled into the library
+ *                   (gf_bitslice.hpp: k in {3,4,6,8,10,12}, m <= 5) where k + m > 9;
+ *   BLBRS_NET_TILE  the fused encode+CRC tile kernel (k + m > 11);
+ *   BLBRS_NET_PACK  PackTracts + Encode (k + m > 9);
+ *   BLBRS_NET_RTC   rs_code_kernel with a network generated and compiled at run time (rtc.hpp:
+ *                   k outside the compiled list, k + m > BLBRS_RTC_WIDE).
+ * 0 = tables everywhere (also with the knob BLBRS_BITSLICE = 0).  Same bytes either way; a
  * diagnostic for tests and profiles. */
+#define BLBRS_NET_CODE 1
+#define BLBRS_NET_TILE 2
+#define BLBRS_NET_PACK 4
+#define BLBRS_NET_RTC  8
 int blbrs_encoder_compiled_network(const blbrs_encoder* enc);
 
 /* ---- host-memory Encoder methods (what the cgo shim binds) ---- */
@@ -397,6 +406,54 @@ int blbrs_pack_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_str
 int blbrs_set_device(int device);      /* hipSetDevice for the calling thread (the library
                                           itself never relies on it) */
 int blbrs_device_count(int* count);
+/* ---- NUMA placement (8-GPU hosts: two sockets, four GPUs behind each) ----
+ * A host call on pool or registered buffers prefers a GPU attached to the NUMA node holding the
+ * shards (recorded once per buffer), the least-loaded such lane unless it carries more than
+ * 64 MiB beyond the least-loaded lane overall; other memory is routed by load alone. */
+/* The node of a device's PCIe root (sysfs), -1 when unknown. */
+int blbrs_device_numa_node(int device, int* node);
+/* Override it (containers without sysfs; tests). */
+int blbrs_set_device_numa_node(int device, int node);
+/* The node recorded for the pool or registered buffer containing p, else -1. */
+int blbrs_host_numa_node(const void* p, int* node);
+/* The routing policy over explicit lane nodes and bytes in flight, scanning from `start`: the
+ * lane index it picks for host shards on `node` (-1: none).  For tests and tools. */
+int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t start, int node, size_t* lane);
+
+/* ---- A/B knobs and run-time networks ---- */
+
+/* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_OCC_LDS, BLBRS_OCC_LDS_ECT,
+ * BLBRS_PACK_VARIANT, BLBRS_PE_CM_WIDE, BLBRS_HOST_ZC, BLBRS_EC_PERSISTENT, BLBRS_EC_FLAGS,
+ * BLBRS_RTC, BLBRS_RTC_CSE, BLBRS_RTC_WIDE) start from the environment, read
+ * once, and change only here -- never by setenv while the library runs.  INVALID_ARG for an
+ * unknown name. */
+int blbrs_set_tuning(const char* name, long value);
+int blbrs_get_tuning(const char* name, long* value);
+
+/* Decode networks generated per erasure pattern and compiled with hipRTC.
+ * A wide decode pass (k + rows > BLBRS_RTC_WIDE) requests its network on first use; with
+ * BLBRS_RTC = 1 (default) it compiles in the background and the pass runs the table kernel until
+ * the network is loaded, with BLBRS_RTC = 2 the first call compiles it, 0 disables them. */
+typedef struct {
+    uint64_t requested;  /* networks requested (one per pass, mode, addressing, device) */
+    uint64_t compiled;   /* distinct sources compiled */
+    uint64_t loaded;     /* kernels loaded on a device */
+    uint64_t failed;     /* compile or load failures (those passes stay on tables) */
+    uint64_t pending;    /* queued, not yet loaded */
+    double compile_ms;   /* total compile time */
+} blbrs_rtc_stats;
+int blbrs_rtc_get_stats(blbrs_rtc_stats* out);
+/* Compiles (without loading; no device needed) the network kernel of rows x k coefficients in
+ * mode 0 store / 1 verify / 2 store+verify, strided or pointer-table addressing: BLBRS_OK, or
+ * BLBRS_ERR_HIP with the compiler log in blbrs_last_error().  For tests. */
+int blbrs_rtc_compile(int k, int rows, const uint8_t* coef, int mode, int strided);
+/* Waits until no network is queued or compiling (timeout_ms < 0: no limit).  BLBRS_OK when idle,
+ * BLBRS_ERR_LIMIT on timeout. */
+int blbrs_rtc_wait(long timeout_ms);
+/* The generated network (device source) for rows x k coefficients, NUL-terminated into out
+ * (cap bytes); *ops = its VALU ops per 8-dword group.  INVALID_ARG when cap is too small. */
+int blbrs_rtc_network_source(int k, int rows, const uint8_t* coef, int cse, char* out, size_t cap, int* ops);
+
 const char* blbrs_last_error(void);    /* thread-local message for the last failure */
 const char* blbrs_version(void);
 const char* blbrs_strerror(int code);

@@ -12,6 +12,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libblbrs.so on the GPU)")
 
 
+@pytest.fixture
+def knob():
+    """knob(name, value): set a library tuning knob (blbrs_set_tuning; the library reads the
+    environment only once) for this test; every knob touched is restored afterwards."""
+    from blb_amd import reedsolomon as rs
+    old = {}
+
+    def set_(name, value):
+        if name not in old:
+            old[name] = rs.get_tuning(name)
+        rs.set_tuning(name, int(value))
+    yield set_
+    for name, value in old.items():
+        rs.set_tuning(name, value)
+
+
 @pytest.fixture(scope="session")
 def oracle_lib():
     from oracle import oracle as O

@@ -1,6 +1,6 @@
 """The compiled bit-plane encode network (gf_bitslice.hpp) against the oracle and against the
-v_perm table path it replaces for encode passes.  BLBRS_BITSLICE (read per launch) = 2 puts
-every compiled shape on the network (by default only k + m > 9), = 0 on the tables.
+v_perm table path it replaces for encode passes.  The knob BLBRS_BITSLICE (blbrs_set_tuning) = 2
+puts every compiled shape on the network (by default only k + m > 9), = 0 on the tables.
 
 Every compiled shape (k in {3, 4, 6, 8, 10, 12}, m = 1..5) runs through the four kernels that
 carry the network -- rs_code_kernel in store and verify mode, the fused encode+CRC tile kernel
@@ -29,15 +29,15 @@ def _oracle_parity(O, k, m, data):
 
 
 @pytest.mark.parametrize("k,m", SHAPES)
-def test_network_encode_verify_vs_oracle_and_tables(oracle_lib, k, m, monkeypatch):
+def test_network_encode_verify_vs_oracle_and_tables(oracle_lib, k, m, knob):
     # 3 whole 16 KiB tiles + a ragged tail: network tiles and table tiles in one launch
     S, B = 3 * 16384 + 4 * 1000 + 12, 3
     rng = np.random.default_rng(1000 * k + m)
     host = rng.integers(0, 256, (B, k + m, S), dtype=np.uint8)
     host[:, k:] = 0xEE
-    monkeypatch.setenv("BLBRS_BITSLICE", "2")
+    knob("BLBRS_BITSLICE", 2)
     enc = rs.New(k, m)
-    assert enc.compiled_network()
+    assert enc.compiled_network()["code"]
     st = torch.from_numpy(host).cuda()
     enc.EncodeBatch(st)
     got = st.cpu().numpy()
@@ -51,8 +51,8 @@ def test_network_encode_verify_vs_oracle_and_tables(oracle_lib, k, m, monkeypatc
     bad[2, k, S - 3] ^= 0x01               # inside the ragged tail (table path)
     assert enc.VerifyBatch(bad).cpu().tolist() == [True, False, False]
     # the table path writes the same bytes and accepts the network's parity
-    monkeypatch.setenv("BLBRS_BITSLICE", "0")
-    assert not enc.compiled_network()
+    knob("BLBRS_BITSLICE", 0)
+    assert not enc.compiled_network()["code"]
     tab = torch.from_numpy(host).cuda()
     enc.EncodeBatch(tab)
     assert torch.equal(tab, st)
@@ -61,7 +61,7 @@ def test_network_encode_verify_vs_oracle_and_tables(oracle_lib, k, m, monkeypatc
 
 
 @pytest.mark.parametrize("k,m", [(6, 3), (8, 3), (10, 4), (12, 5), (3, 2), (4, 1), (10, 5)])
-def test_network_encode_crc_vs_oracle(oracle_lib, k, m, monkeypatch):
+def test_network_encode_crc_vs_oracle(oracle_lib, k, m, knob):
     """Fused encode + 65532-byte block CRCs: network and table kernels agree with the oracle
     on the parity and on every block CRC (a partial last tile: S % 8 KiB != 0)."""
     S, B = 4 * 65532 + 16 * 37, 2
@@ -71,7 +71,7 @@ def test_network_encode_crc_vs_oracle(oracle_lib, k, m, monkeypatch):
     enc = rs.New(k, m)
     outs = {}
     for mode in ("2", "0"):
-        monkeypatch.setenv("BLBRS_BITSLICE", mode)
+        knob("BLBRS_BITSLICE", int(mode))
         st = torch.from_numpy(host).cuda()
         crc = enc.EncodeBatchCRC(st, 65532).cpu().numpy().view(np.uint32)
         outs[mode] = (st.cpu().numpy(), crc)
@@ -85,7 +85,7 @@ def test_network_encode_crc_vs_oracle(oracle_lib, k, m, monkeypatch):
 
 
 @pytest.mark.parametrize("k,m", [(6, 3), (8, 3), (12, 5), (3, 2), (10, 4)])
-def test_network_pack_encode_vs_tables(k, m, monkeypatch):
+def test_network_pack_encode_vs_tables(k, m, knob):
     """PackTracts + Encode with the network (U = 2 tiles for every k) equals the table kernel
     (U = 1 for k > 6) and Verify accepts the parity; misaligned sources, holes and a ragged
     last tile."""
@@ -105,10 +105,10 @@ def test_network_pack_encode_vs_tables(k, m, monkeypatch):
     enc = rs.New(k, m)
     res = {}
     for mode in ("2", "0"):
-        monkeypatch.setenv("BLBRS_BITSLICE", mode)
+        knob("BLBRS_BITSLICE", int(mode))
         st = torch.full((B, k + m, S), 0x5C, dtype=torch.uint8, device="cuda")
         pack.PackEncode(enc, st, ext)
         res[mode] = st
     assert torch.equal(res["2"], res["0"])
-    monkeypatch.delenv("BLBRS_BITSLICE")
+    knob("BLBRS_BITSLICE", 1)
     assert bool(enc.VerifyBatch(res["2"]).all())

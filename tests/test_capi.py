@@ -108,21 +108,25 @@ def test_c_abi_null_arguments():
     assert b"gfx950" in lib.blbrs_version()
 
 
-def test_compiled_network_covers_blb_classes(monkeypatch):
+def test_compiled_network_covers_blb_classes(knob):
     """The parity rows built into the library (gf_bitslice.hpp, constexpr buildMatrix) equal
     the runtime matrix for every compiled (k, m) -- with BLBRS_BITSLICE=2 Encode / Verify of
-    all 30 shapes run the bit-plane network.  By default only the wide shapes do (k + m > 9,
-    where the table multiply is VALU-bound); other shapes and BLBRS_BITSLICE=0 keep the
-    v_perm table path."""
+    all 30 shapes run the bit-plane network.  By default only the wide shapes do, each kernel
+    with its own threshold (rs_code_kernel and PackTracts + Encode k + m > 9, the fused
+    encode+CRC tile kernel k + m > 11); other shapes and BLBRS_BITSLICE=0 keep the v_perm
+    table path.  Wide k outside the compiled list takes a run-time network (rtc)."""
     from blb_amd import reedsolomon as rs
-    monkeypatch.setenv("BLBRS_BITSLICE", "2")
+    knob("BLBRS_BITSLICE", 2)
     for k in (3, 4, 6, 8, 10, 12):
         for m in range(1, 6):
-            assert rs.New(k, m).compiled_network(), (k, m)
+            assert rs.New(k, m).compiled_network()["code"], (k, m)
     for k, m in ((5, 3), (10, 6), (2, 2), (20, 4)):
-        assert not rs.New(k, m).compiled_network(), (k, m)
-    monkeypatch.delenv("BLBRS_BITSLICE")
-    assert [rs.New(k, m).compiled_network() for k, m in ((12, 5), (10, 4), (8, 3), (6, 3), (3, 2))] == \
-        [True, True, True, False, False]
-    monkeypatch.setenv("BLBRS_BITSLICE", "0")
-    assert not rs.New(12, 5).compiled_network()
+        assert not rs.New(k, m).compiled_network()["code"], (k, m)
+    knob("BLBRS_BITSLICE", 1)
+    nets = {(k, m): rs.New(k, m).compiled_network() for k, m in ((12, 5), (10, 4), (8, 3), (6, 3), (3, 2), (14, 4))}
+    assert [nets[s]["code"] for s in ((12, 5), (10, 4), (8, 3), (6, 3), (3, 2))] == [True, True, True, False, False]
+    assert [nets[s]["tile"] for s in ((12, 5), (10, 4), (8, 3), (6, 3))] == [True, True, False, False]
+    assert [nets[s]["pack"] for s in ((12, 5), (10, 4), (8, 3), (6, 3))] == [True, True, True, False]
+    assert nets[(14, 4)] == {"code": False, "tile": False, "pack": False, "rtc": True}
+    knob("BLBRS_BITSLICE", 0)
+    assert not any(rs.New(12, 5).compiled_network().values())

@@ -89,13 +89,12 @@ def test_encode_crc_matches_separate_passes():
         assert torch.equal(crc[j], sep), j
 
 
-def test_encode_crc_tile_grid_cases(oracle_lib):
+def test_encode_crc_tile_grid_cases(oracle_lib, knob):
     """Shapes the tile-grid kernel (encode_crc_tile.hip) takes: rows <= 4, S a whole number
     of 8 KiB tiles, 16-byte aligned strides, block >= tile.  Block boundaries at many dword
     phases inside a tile (block = tile, tile + 4, 2*tile - 4, 65532), whole-shard frames,
     blocks longer than S, and the last short block; each case is also run on the persistent
-    segment kernel (BLBRS_EC_PERSISTENT, read per call)."""
-    import os
+    segment kernel (knob BLBRS_EC_PERSISTENT)."""
     T = 8192
     cases = [(6, 3, 128 * T, 65532, 3, 0), (6, 3, 16 * T, T, 2, 16), (6, 3, 16 * T, T + 4, 2, 32),
              (6, 3, 12 * T, 2 * T - 4, 2, 48), (6, 3, 8 * T, 0, 3, 0), (6, 3, 8 * T, 20 * T, 2, 16),
@@ -104,11 +103,9 @@ def test_encode_crc_tile_grid_cases(oracle_lib):
              (12, 4, 8 * T, T + 4, 2, 0), (10, 3, 5 * T, 0, 2, 0), (12, 5, 8 * T, 65532, 2, 0)]
     for i, (k, m, S, block, B, pad) in enumerate(cases):
         run_case(oracle_lib, k, m, S, block, B=B, pad=pad, seed=100 + i)
-        os.environ["BLBRS_EC_PERSISTENT"] = "1"
-        try:
-            run_case(oracle_lib, k, m, S, block, B=B, pad=pad, seed=200 + i)
-        finally:
-            del os.environ["BLBRS_EC_PERSISTENT"]
+        knob("BLBRS_EC_PERSISTENT", 1)
+        run_case(oracle_lib, k, m, S, block, B=B, pad=pad, seed=200 + i)
+        knob("BLBRS_EC_PERSISTENT", 0)
 
 
 def _expected_blocks_at(O, buf, block, phase, seed):

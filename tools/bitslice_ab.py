@@ -19,7 +19,7 @@ p.add_argument("--shapes", default="6,3,1024;8,3,512;10,4,512;12,5,512")
 p.add_argument("--reps", type=int, default=3)
 p.add_argument("--iters", type=int, default=5)
 p.add_argument("--ops", default="encode,verify,encode_crc")
-# name:VAR=v+VAR2=w;... -- environment of each variant (read per launch by the library)
+# name:VAR=v+VAR2=w;... -- library knobs of each variant (rs.use_knobs / blbrs_set_tuning)
 p.add_argument("--variants", default="net:BLBRS_BITSLICE=2;perm:BLBRS_BITSLICE=0;policy:BLBRS_BITSLICE=1")
 a = p.parse_args()
 dev = torch.device("cuda:0")
@@ -78,18 +78,17 @@ for spec in a.shapes.split(";"):
     res = {}
     for rep in range(a.reps):
         for vname, env in variants:
-            os.environ.update(env)
+            rs.use_knobs(env)
             for name in a.ops.split(","):
                 ms = ops[name]() if name == "pack_encode" else timed(ops[name])
                 res.setdefault(f"{name}_{vname}", []).append(round(ms, 3))
-            for key in env:
-                os.environ.pop(key, None)
+            rs.use_knobs({})
     # the two paths write the same parity
     enc.EncodeBatch(stripes)
     ok = bool(enc.VerifyBatch(stripes).all())
-    os.environ["BLBRS_BITSLICE"] = "0"
+    rs.use_knobs({"BLBRS_BITSLICE": 0})
     ok_perm = bool(enc.VerifyBatch(stripes).all())
-    os.environ.pop("BLBRS_BITSLICE", None)
+    rs.use_knobs({})
     gb = B * (k + m) * S / 1e9
     best = {key: min(v) for key, v in res.items()}
     print(json.dumps({"k": k, "m": m, "B": B, "GB": round(gb, 2), "verify_ok": [ok, ok_perm],

@@ -37,9 +37,7 @@ present = [i != 1 for i in range(k + m)]
 
 
 def setenv(env):
-    for key in knobs:
-        os.environ.pop(key, None)
-    os.environ.update(env)
+    rs.use_knobs(env)  # library knobs (blbrs_set_tuning), read by the library once
 
 
 ok, res = {}, {n: [] for n, _ in variants}

@@ -37,11 +37,11 @@ def main():
               f"crc65532 {t_crc:.3f} ms, sum {t_enc + t_crc:.3f} ms", flush=True)
         for rep in range(2):
             for fl in flags_list:
-                os.environ["BLBRS_EC_FLAGS"] = str(fl)
+                rs.set_tuning("BLBRS_EC_FLAGS", fl)
                 for blk in ((65532, 0) if not fl & 8 else (0,)):
                     t = timeit(lambda: enc.EncodeBatchCRC(st, blk))
                     print(f"  rep{rep} flags={fl} block={blk}: {t:.3f} ms ({algo / t / 1e6:.0f} GB/s)", flush=True)
-        os.environ.pop("BLBRS_EC_FLAGS", None)
+        rs.set_tuning("BLBRS_EC_FLAGS", 0)
         del st, views
         torch.cuda.empty_cache()
 

@@ -44,12 +44,11 @@ for rep in range(a.reps):
     res.setdefault("encode", []).append(timed(lambda: enc.EncodeBatch(stripes)))
     for name, env in variants:
         for blk_name, blk in (("b65532", 65532), ("whole", 0)):
-            os.environ.update(env)
+            rs.use_knobs(env)
             try:
                 ms = timed(lambda: enc.EncodeBatchCRC(stripes, blk))
             finally:
-                for key in env:
-                    del os.environ[key]
+                rs.use_knobs({})
             res.setdefault(f"{name}_{blk_name}", []).append(ms)
     # file-aligned window (rsEncodeOne's parity window at 4 MiB: phase 256) with seeds
     seeds = torch.zeros((m, B), dtype=torch.int32, device=dev)

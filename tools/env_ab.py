@@ -31,9 +31,7 @@ knobs = {key for _, env in variants for key in env}
 
 
 def setenv(env):
-    for key in knobs:
-        os.environ.pop(key, None)
-    os.environ.update(env)
+    rs.use_knobs(env)  # library knobs (blbrs_set_tuning), read by the library once
 
 
 st = torch.empty((B, k + m, S), dtype=torch.uint8, device=dev)

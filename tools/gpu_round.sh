@@ -1,15 +1,65 @@
 #!/bin/bash
-# Round validation on one MI355X: GPU parity suite, smoke(), bench line, rocprof kernel stats.
-# Every GPU step has its own time limit; steps are chained with && so the first failure ends it.
+# The one GPU driver: runs the named steps on one MI355X, each under its own time limit, chained
+# so that the first failure ends the call (no GPU step runs after a failed, killed or faulted one).
+#
+# usage: tools/gpu_round.sh OUT STEPS [TAG] [COMMIT]
+#   OUT    directory under gpurun_out/
+#   STEPS  comma list, run in order:
+#            tests        python -m pytest tests -m gpu (whole GPU suite)
+#            tests:PATHS  the GPU tests of PATHS only ("tests/test_rtc.py tests/test_pack.py")
+#            smoke        __graft_entry__.smoke()
+#            pmc          tools/pmc_prod.sh: FETCH_SIZE / WRITE_SIZE / SQ passes + kernel trace of the
+#                         shipped library -> profiles-ready summary (TAG, COMMIT)
+#            bench        python bench.py (default flags) -> bench.json
+#            rocprof      rocprofv3 --kernel-trace --stats of bench.py --steps 10 --no-extra
+#            ab:CMD       an A/B or measurement driver, e.g. "ab:tools/rpc_shapes.py --reps 5"
+#            probe:ARGS   tools/_build/mix_probe ARGS
+# e.g. gpurun -- 'bash tools/gpu_round.sh r4val tests,smoke,bench,rocprof'
 set -o pipefail
-OUT=gpurun_out/${1:-val}
+OUT=gpurun_out/${1:?out}
+STEPS=${2:?steps}
+TAG=${3:-r04}
+COMMIT=${4:-unknown}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 ROOT=$(pwd)
-echo "== pytest -m gpu" && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
-&& echo "== smoke" && timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
-&& echo "== bench" && timeout -k 10 420 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
-&& echo "== rocprof" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-extra > "$OUT/prof.log" 2>&1
-rc=$?
-echo "exit $rc"; tail -3 "$OUT/pytest_gpu.log"; cat "$OUT/smoke.log"; cat "$OUT/bench.json"
-exit $rc
+IFS=',' read -ra LIST <<< "$STEPS"
+n=0
+for step in "${LIST[@]}"; do
+  n=$((n + 1))
+  echo "== $step"
+  case "$step" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+      rc=$?; tail -3 "$OUT/pytest_gpu.log" ;;
+    tests:*)
+      timeout -k 10 600 python -u -m pytest ${step#tests:} -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu_$n.log" 2>&1
+      rc=$?; tail -3 "$OUT/pytest_gpu_$n.log" ;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      rc=$?; cat "$OUT/smoke.log" ;;
+    pmc)
+      bash tools/pmc_prod.sh "$OUT/pmc" "$TAG" "$COMMIT" > "$OUT/pmc.log" 2>&1
+      rc=$?; tail -2 "$OUT/pmc.log" | cut -c1-800 ;;
+    bench)
+      timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+      rc=$?; cut -c1-1500 "$OUT/bench.json" ;;
+    rocprof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o bench -- \
+        python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-extra > "$OUT/prof.log" 2>&1
+      rc=$?; tail -2 "$OUT/prof.log" ;;
+    ab:*)
+      timeout -k 10 900 python -u ${step#ab:} > "$OUT/ab_$n.jsonl" 2> "$OUT/ab_$n.err"
+      rc=$?; cut -c1-3000 "$OUT/ab_$n.jsonl"; tail -3 "$OUT/ab_$n.err" ;;
+    probe:*)
+      timeout -k 10 300 tools/_build/mix_probe ${step#probe:} > "$OUT/probe_$n.txt" 2>&1
+      rc=$?; cat "$OUT/probe_$n.txt" ;;
+    *)
+      echo "unknown step $step"; rc=2 ;;
+  esac
+  if [ $rc -ne 0 ]; then
+    echo "step $step failed: exit $rc"
+    exit $rc
+  fi
+done
+echo "all steps ok"

@@ -5,7 +5,9 @@
     (4 MiB, internal/tractserver/config.go:117) and at a full 8 MiB tract, next to the CPU
     oracle doing the same call;
   * per-call Encode / ReconstructData on shards from the pinned buffer pool
-    (blbrs_buffer_get = rpc.GetBuffer, pkg/rpc/pool.go) from 1..16 concurrent threads, the
+    (blbrs_buffer_get: library-owned pinned buffers, allocated once and reused -- not the
+    registered caller memory the shipped rpc.GetBuffer drop-in hands out; bench.py's
+    rpc_pool_extras measures that path, pkg/rpc/pool.go) from 1..16 concurrent threads, the
     way concurrent RSEncode RPCs (internal/tractserver/store.go:1099) and degraded reads
     (client/blb/reconstruct.go:173) call it, with and without a Batcher attached (concurrent
     calls share launches).
@@ -47,16 +49,13 @@ def main():
     dev = torch.device("cuda:0")
     out = {}
     if "--zc-sweep" in sys.argv:
-        # Zero-copy vs DMA staging of pinned shards (BLBRS_HOST_ZC, read per call), and the
-        # library's default policy, on the pool-buffer calls and the client shape.
+        # Zero-copy vs DMA staging of pinned shards (knob BLBRS_HOST_ZC), and the library's
+        # default policy (-1), on the pool-buffer calls and the client shape.
         for mode in ("1", "0", "auto"):
-            if mode == "auto":
-                os.environ.pop("BLBRS_HOST_ZC", None)
-            else:
-                os.environ["BLBRS_HOST_ZC"] = mode
+            rs.set_tuning("BLBRS_HOST_ZC", -1 if mode == "auto" else int(mode))
             out[f"zc_{mode}"] = {"pool_calls": pool_calls(6, 3, seconds=1.0), "client_shape": client_shape(6, 3, 1.0)}
             print(json.dumps({mode: out[f"zc_{mode}"]}), file=sys.stderr, flush=True)
-        os.environ.pop("BLBRS_HOST_ZC", None)
+        rs.set_tuning("BLBRS_HOST_ZC", -1)
         print(json.dumps(out))
         return
     if "--client-only" in sys.argv:
@@ -137,8 +136,8 @@ def main():
 
 
 def client_shape(k, m, seconds=1.5):
-    """reconstructOneTract's call: data[i] = pool-buffer replies (rpc.GetBuffer ->
-    blbrs_buffer_get, pinned), data[target] = thisB[0:0:length], a slice of the user's
+    """reconstructOneTract's call: data[i] = pool-buffer replies (library-owned
+    pinned buffers from blbrs_buffer_get, standing in for rpc.GetBuffer's registered ones), data[target] = thisB[0:0:length], a slice of the user's
     pageable buffer; ReconstructData.  T threads, each its own stripe; GiB/s of data (k
     pieces per call)."""
     res = {}

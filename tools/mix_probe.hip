@@ -121,6 +121,29 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 1 && std::string(argv[1]) == "rpc") {
+        // blb's recovery shapes (tools/rpc_shapes.py): the RPC reads k and writes m (every
+        // absent slot rebuilt), the client reads k and writes 1..m.  B as in rpc_shapes.py.
+        CK(hipMalloc(&g_src, size_t(6400) * S + 64));  // max B*R: 640*10
+        CK(hipMalloc(&g_dst, size_t(3072) * S));       // max B*W: 1024*3
+        CK(hipMemset(g_src, 0x3C, size_t(6400) * S + 64));
+        for (int rep = 0; rep < 2; ++rep) {
+            printf("# rep %d\n", rep);
+            run<6, 3, 4, false>(1024);  // RS(6,3)
+            run<6, 1, 4, false>(1024);
+            run<8, 3, 2, false>(768);   // RS(8,3)
+            run<8, 3, 4, false>(768);
+            run<8, 1, 4, false>(768);
+            run<10, 3, 2, false>(640);  // RS(10,3)
+            run<10, 1, 2, false>(640);
+            run<10, 1, 4, false>(640);
+            run<12, 5, 2, false>(480);  // RS(12,5)
+            run<12, 5, 1, false>(480);
+            run<12, 1, 2, false>(480);
+            run<12, 1, 4, false>(480);
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "rs83") {
         // RS(8,3) pack + encode, bench.py's cold_class_extras: 512 stripes, the tracts fill
         // 5.7 of the 8 data pieces (24.5 GB read), 11 shards written (pieces + parity).

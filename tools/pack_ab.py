@@ -13,6 +13,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from blb_amd import pack  # noqa: E402
+from blb_amd import reedsolomon as rs  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--k", type=int, default=6)
@@ -67,7 +68,7 @@ def run():
 
 
 def timed(v):
-    os.environ["BLBRS_PACK_VARIANT"] = str(v)
+    rs.set_tuning("BLBRS_PACK_VARIANT", v)
     run()
     torch.cuda.synchronize(dev)
     torch.cuda._sleep(400_000_000)  # host-side extent checks outside the window
@@ -83,7 +84,7 @@ def timed(v):
 sums = {}
 for v in variants:
     stripes[:, :k].fill_(0xA5)
-    os.environ["BLBRS_PACK_VARIANT"] = str(v)
+    rs.set_tuning("BLBRS_PACK_VARIANT", v)
     run()
     torch.cuda.synchronize(dev)
     sums[v] = stripes[:, :k].view(torch.int64).sum(dim=-1).cpu()

@@ -62,9 +62,7 @@ knobs = {key for _, env in variants for key in env}
 
 
 def setenv(env):
-    for key in knobs:
-        os.environ.pop(key, None)
-    os.environ.update(env)
+    rs.use_knobs(env)  # library knobs (blbrs_set_tuning), read by the library once
 
 
 res = {n: [] for n, _ in variants}

@@ -4,8 +4,9 @@ production libblbrs.so) into profiles/pmc_<tag>.json.
 Calibration comes from the same process: torch's 8 GiB copy_ reads and writes exactly 8 GiB,
 which gives the FETCH_SIZE and WRITE_SIZE scale factors (MI355X_MICROARCH.md §HBM: on gfx950
 FETCH_SIZE reports 1/2 of wide streaming reads; measured, not assumed).  Per hot-path
-dispatch: corrected HBM read / write bytes next to the algorithmic bytes, the SQ counters of
-the same dispatch, and the kernel-trace average duration.  bench.py uses the encode's bytes
+op (tools/pmc_prod.py: one warm-up launch, then REPS launches): corrected HBM read / write
+bytes next to the algorithmic bytes, the SQ counters and the kernel-trace duration, each the
+mean over the REPS warm launches.  bench.py uses the encode's bytes
 as roofline.traffic only while profiles/pmc_*.json's lib_sha256 equals the loaded library's.
 
 usage: python tools/pmc_prod_summary.py OUTDIR TAG COMMIT
@@ -36,13 +37,6 @@ def dispatches(d, counter=None):
     return [(k, v[0], v[1]) for k, v in sorted(out.items())]
 
 
-def pick(ds, needle, nth=0):
-    hits = [x for x in ds if needle in x[1]]
-    if len(hits) <= nth:
-        raise SystemExit(f"no dispatch #{nth} matching {needle!r}")
-    return hits[nth]
-
-
 def csv_in(out, name, kind):
     hits = glob.glob(os.path.join(out, name, "**", f"*{kind}.csv"), recursive=True)
     if not hits:
@@ -59,54 +53,62 @@ def main():
     fetch = dispatches(rows(csv_in(out, "fetch", "counter_collection")))
     write = dispatches(rows(csv_in(out, "write", "counter_collection")))
     sq = dispatches(rows(csv_in(out, "sq", "counter_collection")))
-    trace = rows(csv_in(out, "trace", "kernel_trace"))
-    k, m, B, S = meta["k"], meta["m"], meta["batch"], meta["shard"]
+    trace = sorted(rows(csv_in(out, "trace", "kernel_trace")), key=lambda r: int(r["Dispatch_Id"]))
 
     # calibration: the copy kernel that follows the fill (both 8 GiB)
-    big = [x for x in fetch if not any(n in x[1] for n in ("rs_code", "encode_crc", "crc_stream", "pack_kernel"))]
+    needles = {o["needle"] for o in meta["plan"]}
+    big = [x for x in fetch if not any(n in x[1] for n in needles | {"tile_combine", "tile_chunk"})]
     copy_f = max(big, key=lambda x: x[2].get("FETCH_SIZE", 0.0))
     f_scale = 8 * GIB / (copy_f[2]["FETCH_SIZE"] * 1024.0)
     bigw = [x for x in write if x[0] == copy_f[0]]
     w_scale = 8 * GIB / (bigw[0][2]["WRITE_SIZE"] * 1024.0)
 
-    def durations(needle, nth=0):
-        ts = [r for r in trace if needle in r["Kernel_Name"]]
-        if len(ts) <= nth:
-            return None
-        r = ts[nth]
-        return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # ms
+    def consume(seq, names, plan):
+        """Walk the dispatches in order: each op takes the next `launches` whose kernel name
+        contains its needle; the first is the warm-up.  Returns {label: [timed entries]}."""
+        out, pos = {}, 0
+        for o in plan:
+            got = []
+            while len(got) < o["launches"]:
+                if pos >= len(seq):
+                    raise SystemExit(f"ran out of dispatches at {o['label']}")
+                if o["needle"] in names(seq[pos]):
+                    got.append(seq[pos])
+                pos += 1
+            out[o["label"]] = got[1:]
+        return out
+
+    f_ops = consume(fetch, lambda x: x[1], meta["plan"])
+    w_ops = consume(write, lambda x: x[1], meta["plan"])
+    s_ops = consume(sq, lambda x: x[1], meta["plan"])
+    t_ops = consume(trace, lambda r: r["Kernel_Name"], meta["plan"])
+
+    def mean(vals):
+        return sum(vals) / len(vals) if vals else None
 
     kernels = {}
-    spec = [("encode", "rs_code_kernel", 0, B * (k + m) * S),
-            ("reconstruct_data1", "rs_code_kernel", 1, B * (k + 1) * S),
-            ("verify", "rs_code_kernel", 2, B * (k + m) * S),
-            ("encode_crc_65532", "encode_crc_tile_kernel", 0, B * (k + m) * S),
-            ("encode_crc_combine", "tile_combine_kernel", 0, None),
-            ("crc32c_65532", "crc_stream_kernel", 0, B * S)]
-    if meta.get("pack"):
-        spec.append(("pack_tracts", "pack_kernel", 0, meta["pack"]["bytes_read"] + meta["pack"]["bytes_written"]))
-    wide = meta.get("wide")
-    if wide:  # RS(12,5) on the compiled network: dispatches after the RS(6,3) ones
-        wb = wide["batch"] * (wide["k"] + wide["m"]) * S
-        spec += [("encode_rs12_5_network", "rs_code_kernel", 3, wb),
-                 ("encode_crc_rs12_5_network", "encode_crc_tile_kernel", 1, wb),
-                 ("verify_rs12_5_network", "rs_code_kernel", 4, wb)]
-    for label, needle, nth, algo in spec:
-        f = pick(fetch, needle, nth)
-        w = pick(write, needle, nth)
-        s = pick(sq, needle, nth)
-        rd = f[2]["FETCH_SIZE"] * 1024.0 * f_scale
-        wr = w[2]["WRITE_SIZE"] * 1024.0 * w_scale
-        e = {"kernel": f[1], "hbm_read_bytes": round(rd), "hbm_write_bytes": round(wr),
+    for o in meta["plan"]:
+        label, algo = o["label"], o["algorithmic_bytes"]
+        rd = mean([x[2]["FETCH_SIZE"] for x in f_ops[label]]) * 1024.0 * f_scale
+        wr = mean([x[2]["WRITE_SIZE"] for x in w_ops[label]]) * 1024.0 * w_scale
+        counters = sorted({c for x in s_ops[label] for c in x[2]})
+        sqv = {c: mean([x[2].get(c, 0.0) for x in s_ops[label]]) for c in counters}
+        ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in t_ops[label]]
+        e = {"kernel": f_ops[label][0][1], "launches_averaged": len(ms),
+             "hbm_read_bytes": round(rd), "hbm_write_bytes": round(wr),
              "hbm_bytes": round(rd + wr), "algorithmic_bytes": algo,
              "traffic_over_algorithmic": round((rd + wr) / algo, 6) if algo else None,
-             "trace_ms": durations(needle, nth), "sq": s[2]}
-        sqv = s[2]
+             "trace_ms": round(mean(ms), 4), "trace_ms_each": [round(x, 4) for x in ms], "sq": sqv}
         if sqv.get("SQ_LDS_IDX_ACTIVE"):
             e["lds_bank_conflict_frac"] = round(sqv.get("SQ_LDS_BANK_CONFLICT", 0) / sqv["SQ_LDS_IDX_ACTIVE"], 4)
+        if sqv.get("SQ_WAVES"):
+            e["valu_insts_per_wave"] = round(sqv.get("SQ_INSTS_VALU", 0) / sqv["SQ_WAVES"], 1)
         kernels[label] = e
+    k, m, B, S = meta["k"], meta["m"], meta["batch"], meta["shard"]
+    wide = meta.get("wide")
     res = {"tag": tag, "commit": commit, "lib_sha256": meta["lib_sha256"],
            "workload": {"k": k, "m": m, "batch": B, "shard": S, "wide": wide},
+           "reps": meta.get("reps"), "rtc": meta.get("rtc"),
            "calibration": {"kernel": copy_f[1], "bytes_each_way": 8 * GIB,
                            "fetch_size_scale": round(f_scale, 4), "write_size_scale": round(w_scale, 4)},
            "hbm_bytes_per_launch": kernels["encode"]["hbm_bytes"],
