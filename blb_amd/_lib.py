@@ -77,7 +77,7 @@ SIGNATURES = {
     "blbrs_set_tuning": (_I, [ctypes.c_char_p, ctypes.c_long]),
     "blbrs_get_tuning": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_long)]),
     "blbrs_rtc_get_stats": (_I, [_P]),
-    "blbrs_rtc_compile": (_I, [_I, _I, _P, _I, _I]),
+    "blbrs_rtc_compile": (_I, [_I, _I, _P, _I, _I, _P, _SZ, ctypes.POINTER(_SZ)]),
     "blbrs_rtc_wait": (_I, [ctypes.c_long]),
     "blbrs_rtc_network_source": (_I, [_I, _I, _P, _I, _P, _SZ, ctypes.POINTER(_I)]),
     "blbrs_last_error": (ctypes.c_char_p, []),

@@ -391,11 +391,14 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         const bool aot = bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode) &&  // compiled encode network
                          tune::get(tune::kRtcEncode) == 0;
         if (!aot && bs::mode() != 0 && rtc::eligible(ps.k_in, ps.rows)) {
-            auto& slot = ps.net->k[static_cast<int>(m)][st.base ? 0 : 1];
+            const int mi = static_cast<int>(m), ai = st.base ? 0 : 1;
+            auto& slot = ps.net->k[mi][ai];
+            const unsigned gen = tune::generation();  // knobs (BLBRS_RTC_CSE, _WPE) shape the source
             rtc::NetKernel* nk = slot.load(std::memory_order_acquire);
-            if (!nk) {
+            if (!nk || ps.net->gen[mi][ai].load(std::memory_order_acquire) != gen) {
                 nk = rtc::request(plan.device, ps.k_in, ps.rows, m, st.base != nullptr, ps.coef.data());
                 slot.store(nk, std::memory_order_release);
+                ps.net->gen[mi][ai].store(gen, std::memory_order_release);
             }
             net = nk;
         }
@@ -1134,12 +1137,19 @@ int blbrs_rtc_get_stats(blbrs_rtc_stats* out) {
     return BLBRS_OK;
 }
 
-int blbrs_rtc_compile(int k, int rows, const uint8_t* coef, int mode, int strided) {
+int blbrs_rtc_compile(int k, int rows, const uint8_t* coef, int mode, int strided, void* code, size_t cap,
+                      size_t* len) {
     if (k < 1 || k > 16 || rows < 1 || rows > kMaxRows || !coef || mode < 0 || mode > 2)
         return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
     std::string log;
-    if (!rtc::compile_only(k, rows, static_cast<Mode>(mode), strided != 0, coef, &log))
+    std::vector<char> obj;
+    if (!rtc::compile_only(k, rows, static_cast<Mode>(mode), strided != 0, coef, &log, &obj))
         return fail(BLBRS_ERR_HIP, "hipRTC: " + log.substr(0, 2000));
+    if (len) *len = obj.size();
+    if (code) {
+        if (cap < obj.size()) return fail(BLBRS_ERR_INVALID_ARG, "code buffer too small");
+        std::memcpy(code, obj.data(), obj.size());
+    }
     return BLBRS_OK;
 }
 

@@ -263,11 +263,28 @@ __device__ __forceinline__ void parity_rows(const uint32_t (&x)[K][8], uint32_t 
 // takes every input's planes (x, transposed by the caller) and returns rows 0..MR-1 in byte
 // form.  EncodeNet<K> is the encode matrix compiled into the library; rtc.hip generates the
 // same interface for decode rows.
+// NET::each<MR>(x, f) does the same one row at a time, calling f(r, row) as soon as row r is in
+// byte form, so a store-only caller keeps 8 output registers live instead of 8 * MR.
+template <int K, int R, int MR, class F>
+__device__ __forceinline__ void parity_each(const uint32_t (&x)[K][8], F& f) {
+    if constexpr (R < MR) {
+        uint32_t o[8];
+        row_planes<K, R, 0>(x, o);
+        transpose8(o);
+        f(R, o);
+        parity_each<K, R + 1, MR>(x, f);
+    }
+}
+
 template <int K>
 struct EncodeNet {
     template <int MR>
     __device__ static __forceinline__ void rows(const uint32_t (&x)[K][8], uint32_t (&out)[MR][8]) {
         parity_rows<K, MR>(x, out);
+    }
+    template <int MR, class F>
+    __device__ static __forceinline__ void each(const uint32_t (&x)[K][8], F& f) {
+        parity_each<K, 0, MR>(x, f);
     }
 };
 
@@ -277,10 +294,16 @@ struct NetRows {
     __device__ static __forceinline__ void run(const uint32_t (&x)[K][8], uint32_t (&out)[MR][8]) {
         NET::template rows<MR>(x, out);
     }
+    template <class F>
+    __device__ static __forceinline__ void each(const uint32_t (&x)[K][8], F& f) {
+        NET::template each<MR>(x, f);
+    }
 };
 template <int K, int MR>
 struct NetRows<void, K, MR> {
     __device__ static __forceinline__ void run(const uint32_t (&)[K][8], uint32_t (&)[MR][8]) {}
+    template <class F>
+    __device__ static __forceinline__ void each(const uint32_t (&)[K][8], F&) {}
 };
 
 // acc ^ the terms [J, n) of input group GI for parity row R, output bit P (x: every input's

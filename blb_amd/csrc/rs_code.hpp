@@ -42,6 +42,11 @@
 #ifndef BLBRS_CM_GROUP_LOADS
 #define BLBRS_CM_GROUP_LOADS 1
 #endif
+// 1 = store mode writes each network row as soon as it is formed (NET::each); 0 = all rows, then
+// the stores.
+#ifndef BLBRS_CM_ROW_STORES
+#define BLBRS_CM_ROW_STORES 1
+#endif
 
 namespace blbrs {
 namespace code {
@@ -145,8 +150,17 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
 template <class T> struct is_void { static constexpr bool value = false; };
 template <> struct is_void<void> { static constexpr bool value = true; };
 
+// BLBRS_NET_WPE > 0: network kernels of k + rows <= 14 ask the compiler for that many waves per
+// SIMD (RS(10,x) networks otherwise land at 129-130 VGPRs, one over the 4-wave budget).  Off in
+// the library build; run-time networks take it from the knob BLBRS_RTC_WPE (rtc.hip).
+#ifndef BLBRS_NET_WPE
+#define BLBRS_NET_WPE 0
+#endif
+constexpr int net_wpe(int k, int rows, bool cm) { return cm && BLBRS_NET_WPE > 0 && k + rows <= 14 ? BLBRS_NET_WPE : 1; }
+
 template <int K, int MR, int MODE, int ADDR, int U, int NT, class NET = void>
-__global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(net_wpe(K, MR, !is_void<NET>::value))))
+void rs_code_kernel(CodeArgs a) {
     constexpr bool CM = !is_void<NET>::value;
     static_assert(!CM || (K > 0 && U % 2 == 0), "network shapes");
     constexpr uint32_t kTile = kTileBytes * U;
@@ -228,6 +242,15 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
                     }
 #pragma unroll
                     for (int c = 0; c < K; ++c) bs::transpose8(xs[c]);
+                    if constexpr (MODE == 0 && BLBRS_CM_GROUP_LOADS && BLBRS_CM_ROW_STORES) {
+                        // each row stored as soon as it is formed: 8 output registers live, not 8 * MR
+                        auto put = [&](int r, const uint32_t (&o)[8]) {
+                            uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
+                            st16<NT>(q + 2 * g * kStep, pack(o));
+                            st16<NT>(q + (2 * g + 1) * kStep, pack(o + 4));
+                        };
+                        bs::NetRows<NET, K, MR>::each(xs, put);
+                    } else {
                     bs::NetRows<NET, K, MR>::run(xs, og);
 #pragma unroll
                     for (int r = 0; r < MR; ++r)
@@ -240,6 +263,7 @@ __global__ __launch_bounds__(kThreads) void rs_code_kernel(CodeArgs a) {
                             st16<NT>(q + 2 * g * kStep, pack(acc[r] + 8 * g));
                             st16<NT>(q + (2 * g + 1) * kStep, pack(acc[r] + 8 * g + 4));
                         }
+                    }
                     }
                 }
             } else {

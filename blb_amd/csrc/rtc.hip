@@ -40,10 +40,14 @@ constexpr size_t kMaxEntries = 512;  // kernels kept per process; past it, passe
 // --- network generation --------------------------------------------------------------------
 
 // Output plane (r, p) = XOR of input planes (c, q) with bit p of coef[r][c] * 2^q set
-// (multiplying by a constant is GF(2)-linear).  With `cse`, a pair of signals that appears in
-// three or more outputs becomes one temporary (greedy, most frequent pair first, temporaries may
-// pair again: Paar's heuristic); an output of T signals then costs ceil((T - 1) / 2) v_bitop3
-// XOR3s and a temporary one XOR.  The cheaper of the two forms is emitted.
+// (multiplying by a constant is GF(2)-linear), emitted as a chain of v_bitop3 XOR3s.  With `cse`
+// (knob BLBRS_RTC_CSE, off by default), a pair of signals that appears in three or more outputs
+// becomes one temporary first (greedy, most frequent pair first, temporaries may pair again:
+// Paar's heuristic); an output of T signals then costs floor(T / 2) XOR3s and a temporary one
+// XOR, and the cheaper form is emitted.  Measured: it does not pay -- LLVM's reassociation
+// already shares terms (the same static VALU count either way), and the long-lived temporaries
+// take RS(12,5)'s recovery kernel from 156 VGPRs to 252-280 (occupancy 3 -> 2 or 1; 7-35 %
+// slower launches, profiles/r04/rtc_ab).
 struct Net {
     int nin = 0;
     std::vector<std::pair<int, int>> temps;  // signal nin + i = first ^ second
@@ -105,6 +109,18 @@ std::string sig_name(const Net& net, int s) {
     return "t" + std::to_string(s - net.nin);
 }
 
+// One output plane: its signals folded by XOR3s.
+std::string fold_expr(const Net& net, const std::vector<int>& s) {
+    if (s.empty()) return "0u";
+    if (s.size() == 1) return sig_name(net, s[0]);
+    if (s.size() == 2) return sig_name(net, s[0]) + " ^ " + sig_name(net, s[1]);
+    std::string e = "xor3(" + sig_name(net, s[0]) + ", " + sig_name(net, s[1]) + ", " + sig_name(net, s[2]) + ")";
+    size_t i = 3;
+    for (; i + 1 < s.size(); i += 2) e = "xor3(" + e + ", " + sig_name(net, s[i]) + ", " + sig_name(net, s[i + 1]) + ")";
+    if (i < s.size()) e = "(" + e + " ^ " + sig_name(net, s[i]) + ")";
+    return e;
+}
+
 std::string emit(const Net& net, int k, int rows) {
     std::string o;
     o += "struct BlbrsNet {\n  template <int MR>\n  __device__ static __forceinline__ void rows(const uint32_t (&x)[" +
@@ -115,24 +131,21 @@ std::string emit(const Net& net, int k, int rows) {
         o += "    const uint32_t t" + std::to_string(i) + " = " + sig_name(net, net.temps[i].first) + " ^ " +
              sig_name(net, net.temps[i].second) + ";\n";
     for (int r = 0; r < rows; ++r)
-        for (int p = 0; p < 8; ++p) {
-            const auto& s = net.outs[r * 8 + p];
-            std::string e;
-            if (s.empty()) {
-                e = "0u";
-            } else if (s.size() == 1) {
-                e = sig_name(net, s[0]);
-            } else if (s.size() == 2) {
-                e = sig_name(net, s[0]) + " ^ " + sig_name(net, s[1]);
-            } else {
-                e = "xor3(" + sig_name(net, s[0]) + ", " + sig_name(net, s[1]) + ", " + sig_name(net, s[2]) + ")";
-                size_t i = 3;
-                for (; i + 1 < s.size(); i += 2) e = "xor3(" + e + ", " + sig_name(net, s[i]) + ", " + sig_name(net, s[i + 1]) + ")";
-                if (i < s.size()) e = "(" + e + " ^ " + sig_name(net, s[i]) + ")";
-            }
-            o += "    o[" + std::to_string(r) + "][" + std::to_string(p) + "] = " + e + ";\n";
-        }
-    o += "#pragma unroll\n    for (int r = 0; r < MR; ++r) blbrs::bs::transpose8(o[r]);\n  }\n};\n";
+        for (int p = 0; p < 8; ++p)
+            o += "    o[" + std::to_string(r) + "][" + std::to_string(p) + "] = " + fold_expr(net, net.outs[r * 8 + p]) + ";\n";
+    o += "#pragma unroll\n    for (int r = 0; r < MR; ++r) blbrs::bs::transpose8(o[r]);\n  }\n";
+    // each<MR>(x, f): the same rows one at a time, f(r, row) as soon as row r is in byte form.
+    o += "  template <int MR, class F>\n  __device__ static __forceinline__ void each(const uint32_t (&x)[" + std::to_string(k) +
+         "][8], F& f) {\n    static_assert(MR == " + std::to_string(rows) + ", \"rows\");\n    using blbrs::dev::xor3;\n";
+    for (size_t i = 0; i < net.temps.size(); ++i)
+        o += "    const uint32_t t" + std::to_string(i) + " = " + sig_name(net, net.temps[i].first) + " ^ " +
+             sig_name(net, net.temps[i].second) + ";\n";
+    for (int r = 0; r < rows; ++r) {
+        o += "    {\n      uint32_t o[8];\n";
+        for (int p = 0; p < 8; ++p) o += "      o[" + std::to_string(p) + "] = " + fold_expr(net, net.outs[r * 8 + p]) + ";\n";
+        o += "      blbrs::bs::transpose8(o);\n      f(" + std::to_string(r) + ", o);\n    }\n";
+    }
+    o += "  }\n};\n";
     return o;
 }
 
@@ -317,21 +330,29 @@ void unit(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::st
           int* ops) {
     const int imode = static_cast<int>(mode), addr = strided ? 0 : 1;
     *u = network_u(k, rows, imode);
-    *src = "#include \"rs_code.hpp\"\n" + kernel_source(k, rows, coef, tune::get(tune::kRtcCse) != 0, ops);
+    const long wpe = tune::get(tune::kRtcWpe);
+    *src = (wpe > 0 ? "#define BLBRS_NET_WPE " + std::to_string(wpe) + "\n" : std::string()) +
+           "#define BLBRS_CM_ROW_STORES " + std::to_string(tune::get(tune::kRtcRowStores) != 0 ? 1 : 0) + "\n" +
+           "#include \"rs_code.hpp\"\n" + kernel_source(k, rows, coef, tune::get(tune::kRtcCse) != 0, ops);
     *name = "blbrs::code::rs_code_kernel<" + std::to_string(k) + ", " + std::to_string(rows) + ", " +
             std::to_string(imode) + ", " + std::to_string(addr) + ", " + std::to_string(*u) + ", 3, BlbrsNet>";
     *src += "// " + *name + "\n";
 }
 }  // namespace
 
-bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::string* log) {
+bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::string* log,
+                  std::vector<char>* code) {
     std::string src, name;
     int u = 0, ops = 0;
     unit(k, rows, mode, strided, coef, &src, &name, &u, &ops);
     State& s = S();
     {
         std::lock_guard<std::mutex> g(s.mu);
-        if (s.compiled.count(src)) return true;
+        auto it = s.compiled.find(src);
+        if (it != s.compiled.end()) {
+            if (code) *code = it->second->code;
+            return true;
+        }
     }
     const auto t0 = std::chrono::steady_clock::now();
     auto c = compile(src, name, log);
@@ -341,6 +362,7 @@ bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef,
     if (!c) return false;
     ++s.st.compiled;
     s.compiled[src] = c;
+    if (code) *code = c->code;
     return true;
 }
 

@@ -22,6 +22,7 @@
 #include <atomic>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "rs_kernels.hpp"
 
@@ -38,6 +39,7 @@ struct NetKernel {
 // Per-pass lookup cache (mode x addressing), kept in the device plan.
 struct NetSlot {
     std::atomic<NetKernel*> k[3][2] = {};
+    std::atomic<unsigned> gen[3][2] = {};  // tune::generation() the entry was resolved under
 };
 
 // Whether a pass of `rows` rows over `k` inputs may take a run-time network (the knob
@@ -54,7 +56,8 @@ std::string network_source(int k, int rows, const uint8_t* coef, bool cse, int* 
 
 // Compiles the kernel request() would build, without loading it (no device needed); true on
 // success, else false with the compiler log.  Adds to the compile cache.
-bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::string* log);
+bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::string* log,
+                  std::vector<char>* code = nullptr);
 
 struct Stats {
     uint64_t requested = 0, compiled = 0, loaded = 0, failed = 0, pending = 0;

@@ -20,13 +20,20 @@ enum Knob : int {
     kEcPersistent,   // BLBRS_EC_PERSISTENT: fused encode+CRC on the persistent segment kernel (0)
     kEcFlags,        // BLBRS_EC_FLAGS: segment-kernel A/B flags (0)
     kRtc,            // BLBRS_RTC: run-time decode networks 0 = off, 1 = compiled in the background (default), 2 = compiled by the caller
-    kRtcCse,         // BLBRS_RTC_CSE: shared XOR subexpressions in generated networks (1)
-    kRtcWide,        // BLBRS_RTC_WIDE: a decode pass takes a network when k + rows > this (9)
+    kRtcCse,         // BLBRS_RTC_CSE: explicit shared XOR temporaries in generated networks (0: LLVM already
+                     // shares terms; the temporaries raise VGPRs 156 -> 252-280 at RS(12,5))
+    kRtcWide,        // BLBRS_RTC_WIDE: a decode pass takes a network when k + rows > this (13: RS(12,5)-wide
+                     // passes, where the tables are VALU-bound; narrower ones measured +-1-3 %)
     kRtcEncode,      // BLBRS_RTC_ENCODE: encode passes too take run-time networks instead of the compiled ones (0; A/B)
+    kRtcWpe,         // BLBRS_RTC_WPE: waves per SIMD run-time networks of k + rows <= 14 ask for (0 = the compiler's choice)
+    kRtcRowStores,   // BLBRS_RTC_ROW_STORES: run-time networks store each row as it is formed (1) or all rows at the end (0)
     kCount
 };
 
 long get(Knob k);
+// Bumped by every set(): lookups cached under the knobs (run-time network per pass) compare it
+// to notice a change.
+unsigned generation();
 // By BLBRS_* name; false when the name is unknown.
 bool set(const char* name, long value);
 bool get(const char* name, long* value);

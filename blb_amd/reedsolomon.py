@@ -680,12 +680,17 @@ def rtc_network_source(coef: np.ndarray, cse: bool = True) -> tuple[str, int]:
     return buf.value.decode(), int(ops.value)
 
 
-def rtc_compile(coef: np.ndarray, mode: int = 0, strided: bool = True) -> None:
-    """Compile (no device needed) the network kernel of a rows x k coefficient matrix; raises
-    ErrHIP with the compiler log on failure."""
+def rtc_compile(coef: np.ndarray, mode: int = 0, strided: bool = True) -> bytes:
+    """Compile (no device needed) the network kernel of a rows x k coefficient matrix and return
+    its code object (AMDGPU ELF); raises ErrHIP with the compiler log on failure."""
     c = np.ascontiguousarray(coef, dtype=np.uint8)
     rows, k = c.shape
-    _check(_lib.load().blbrs_rtc_compile(k, rows, c.ctypes.data, int(mode), int(strided)))
+    n = ctypes.c_size_t(0)
+    lib = _lib.load()
+    _check(lib.blbrs_rtc_compile(k, rows, c.ctypes.data, int(mode), int(strided), None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value)
+    _check(lib.blbrs_rtc_compile(k, rows, c.ctypes.data, int(mode), int(strided), buf, n.value, ctypes.byref(n)))
+    return buf.raw[:n.value]
 
 
 def version() -> str:

@@ -424,7 +424,8 @@ int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t s
 
 /* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_OCC_LDS, BLBRS_OCC_LDS_ECT,
  * BLBRS_PACK_VARIANT, BLBRS_PE_CM_WIDE, BLBRS_HOST_ZC, BLBRS_EC_PERSISTENT, BLBRS_EC_FLAGS,
- * BLBRS_RTC, BLBRS_RTC_CSE, BLBRS_RTC_WIDE) start from the environment, read
+ * BLBRS_RTC, BLBRS_RTC_CSE, BLBRS_RTC_WIDE, BLBRS_RTC_ENCODE, BLBRS_RTC_WPE,
+ * BLBRS_RTC_ROW_STORES; blb_amd/csrc/tuning.hpp) start from the environment, read
  * once, and change only here -- never by setenv while the library runs.  INVALID_ARG for an
  * unknown name. */
 int blbrs_set_tuning(const char* name, long value);
@@ -445,8 +446,10 @@ typedef struct {
 int blbrs_rtc_get_stats(blbrs_rtc_stats* out);
 /* Compiles (without loading; no device needed) the network kernel of rows x k coefficients in
  * mode 0 store / 1 verify / 2 store+verify, strided or pointer-table addressing: BLBRS_OK, or
- * BLBRS_ERR_HIP with the compiler log in blbrs_last_error().  For tests. */
-int blbrs_rtc_compile(int k, int rows, const uint8_t* coef, int mode, int strided);
+ * BLBRS_ERR_HIP with the compiler log in blbrs_last_error().  The code object (an AMDGPU ELF)
+ * is copied to `code` when non-NULL (cap bytes); *len gets its size.  For tests and tools. */
+int blbrs_rtc_compile(int k, int rows, const uint8_t* coef, int mode, int strided, void* code, size_t cap,
+                      size_t* len);
 /* Waits until no network is queued or compiling (timeout_ms < 0: no limit).  BLBRS_OK when idle,
  * BLBRS_ERR_LIMIT on timeout. */
 int blbrs_rtc_wait(long timeout_ms);

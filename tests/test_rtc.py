@@ -146,6 +146,7 @@ def test_gpu_rpc_and_client_shapes_with_networks(k, m, knob):
     against the oracle; the wide classes must have loaded their networks."""
     torch = _torch()
     knob("BLBRS_RTC", 2)
+    knob("BLBRS_RTC_WIDE", 9)   # networks for every wide class (the default takes k + rows > 13)
     S, B = 3 * 16384 + 4 * 1000 + 16, 3          # whole tiles (network) + a ragged tail (tables)
     host = _oracle_stripes(k, m, B, S, 77 * k + m)
     enc = rs.New(k, m)
@@ -212,6 +213,7 @@ def test_gpu_tractserver_recovery_rpc_with_indexmap_padding(k, m, nbad, knob, or
     from blb_amd.blbcore import Error, RSChunkID, TSAddr
     from blb_amd.tractserver import MemTractserverTalker, Store
     knob("BLBRS_RTC", 2)
+    knob("BLBRS_RTC_WIDE", 9)
     L = 3 * 16384 + 4096 + 16
     host = _oracle_stripes(k, m, 1, L, 5 * k + m)[0]
     hosts = [TSAddr(10 + i, f"ts{i}") for i in range(k + m)]
