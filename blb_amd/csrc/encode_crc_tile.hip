@@ -48,8 +48,10 @@ using namespace dev;
 constexpr int kTThreads = 256;                     // 4 waves, one row each
 constexpr uint64_t kOrd = 0x7FFFFFFFull;            // S_{kOrd} = I (checked on the host)
 // Tuning builds only (tools/ect_variants.sh; the cost split in profiles/r02/ect_ab): 1 = skip
-// the constant staging, 2 = skip the slicing chains, 4 = skip the lane shifts.  Results are
-// wrong with any bit set.
+// the constant staging, 2 = skip the slicing chains, 4 = skip the lane shifts, 16 = the slicing
+// lookups made bank-conflict-free (index = the byte's top 3 bits * 32 + lane % 32: the same
+// instructions and data dependence, one bank per lane of a 32-lane group; profiles/r04/crc_lds).
+// Results are wrong with any bit set.
 #ifndef BLBRS_ECT_FLAGS
 #define BLBRS_ECT_FLAGS 0
 #endif
@@ -195,6 +197,15 @@ __device__ __forceinline__ uint32_t row_totals(const uint32_t* nt, uint32_t lane
 // chunk takes 4 dependent LDS round trips instead of 8 (slicing-by-4: +1.5 % at RS(6,3)).
 __device__ __forceinline__ uint32_t slice8(const uint32_t* tab, uint32_t x, uint32_t y) {
     uint32_t v[8];
+    if constexpr (kFlags & 16) {
+        const uint32_t l32 = threadIdx.x & 31u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = tab[(7 - k) * 256 + ((__builtin_amdgcn_ubfe(x, 8 * k + 5, 3) << 5) | l32)];
+            v[4 + k] = tab[(3 - k) * 256 + ((__builtin_amdgcn_ubfe(y, 8 * k + 5, 3) << 5) | l32)];
+        }
+        return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6]) ^ v[7];
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         v[k] = tab[(7 - k) * 256 + __builtin_amdgcn_ubfe(x, 8 * k, 8)];
