@@ -387,7 +387,7 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         // Wide passes the library has no compiled network for (decode rows; encode rows of k
         // outside the compiled list) take a network generated for their coefficients once it is
         // loaded; until then, and on failure, the table kernel.
-        const rtc::NetKernel* net = nullptr;
+        rtc::NetKernel* net = nullptr;
         const bool aot = bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode) &&  // compiled encode network
                          tune::get(tune::kRtcEncode) == 0;
         if (!aot && bs::mode() != 0 && rtc::eligible(ps.k_in, ps.rows)) {

@@ -107,7 +107,7 @@ unsigned occupancy_lds(bool cm) {
 
 }  // namespace
 
-hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, const rtc::NetKernel* net) {
+hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc::NetKernel* net) {
     if (args.rows < 1 || args.rows > kMaxRows || args.k < 1) return hipErrorInvalidValue;
     if (mode != Mode::kStore && !args.mismatch) return hipErrorInvalidValue;
     if (mode == Mode::kStoreVerify && (args.nstore < 0 || args.nstore > args.rows)) return hipErrorInvalidValue;
@@ -115,7 +115,7 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, cons
     Choice ch = pick(args.k, args.rows, mode, args.base != nullptr, bs::use(args.parity, args.k, args.rows, bs::kWideCode));
     // A run-time network replaces the table kernel once loaded (the caller asks for one only where
     // no compiled encode network applies, or for the BLBRS_RTC_ENCODE A/B).
-    hipFunction_t rfn = net ? net->fn.load(std::memory_order_acquire) : nullptr;
+    hipFunction_t rfn = rtc::ready(net);
     if (rfn) {
         ch.u = net->u;
         ch.cm = true;

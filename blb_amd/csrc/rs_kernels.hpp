@@ -55,7 +55,7 @@ struct NetKernel;
 // Launches one pass over args.B stripes on `stream` (grid, tiles and XCD mapping chosen
 // here); returns hipSuccess or the launch error.  `net`: the pass's run-time network
 // (rtc.hpp), used when loaded, else the ahead-of-time kernel.
-hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, const rtc::NetKernel* net = nullptr);
+hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc::NetKernel* net = nullptr);
 
 // Name of the kernel instantiation launch_code() would pick (for profiling/tests).
 const char* kernel_name(int k, int rows, Mode mode, bool parity = false);

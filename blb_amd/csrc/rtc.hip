@@ -168,6 +168,7 @@ struct State {
     std::map<std::string, std::unique_ptr<NetKernel>> kernels;        // device|source
     std::map<std::string, std::shared_ptr<Compiled>> compiled;        // source
     std::deque<Job> queue;
+    std::mutex load_mu;   // module loads (ready()), one at a time
     bool worker = false;
     int busy = 0;
     bool exiting = false;
@@ -228,7 +229,7 @@ std::shared_ptr<Compiled> compile(const std::string& src, const std::string& nam
     return out;
 }
 
-// Compile if needed, then load on job.device (made current here) and publish the function.
+// Compile if needed and publish the code object (state 2); ready() loads it.  No HIP call.
 void run_job(State& s, const Job& j) {
     std::shared_ptr<Compiled> c;
     {
@@ -249,13 +250,20 @@ void run_job(State& s, const Job& j) {
             return;
         }
         ++s.st.compiled;
-        s.compiled[j.src] = c;
+        s.compiled[j.src] = c;   // entries are never erased: `c` outlives every NetKernel
     }
+    j.nk->code.store(c.get(), std::memory_order_release);
+    j.nk->state.store(2, std::memory_order_release);
+}
+
+// Load a compiled code object on nk->device in this thread (s.load_mu held).
+void load(State& s, NetKernel* nk) {
+    const Compiled* c = static_cast<const Compiled*>(nk->code.load(std::memory_order_acquire));
     int prev = 0;
     (void)hipGetDevice(&prev);
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
-    hipError_t e = hipSetDevice(j.device);
+    hipError_t e = hipSetDevice(nk->device);
     if (e == hipSuccess) e = hipModuleLoadData(&mod, c->code.data());
     if (e == hipSuccess) e = hipModuleGetFunction(&fn, mod, c->lowered.c_str());
     (void)hipSetDevice(prev);
@@ -263,12 +271,12 @@ void run_job(State& s, const Job& j) {
     if (e != hipSuccess || !fn) {
         (void)hipGetLastError();
         note_failure(s, std::string("module load: ") + hipGetErrorString(e));
-        j.nk->state.store(-1);
+        nk->state.store(-1);
         return;
     }
     ++s.st.loaded;
-    j.nk->fn.store(fn);
-    j.nk->state.store(1);
+    nk->fn.store(fn, std::memory_order_release);
+    nk->state.store(1, std::memory_order_release);
 }
 
 void worker_loop() {
@@ -381,6 +389,7 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
         if (it != s.kernels.end()) return it->second.get();
         if (s.exiting || s.kernels.size() >= kMaxEntries) return nullptr;
         auto p = std::make_unique<NetKernel>();
+        p->device = device;
         p->u = u;
         p->ops = ops;
         nk = p.get();
@@ -402,11 +411,22 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
     }
     if (sync) {
         run_job(s, Job{src, name, device, nk});
+        (void)ready(nk);
         std::lock_guard<std::mutex> g(s.mu);
         --s.busy;
         s.cv_idle.notify_all();
     }
     return nk;
+}
+
+hipFunction_t ready(NetKernel* nk) {
+    if (!nk) return nullptr;
+    if (hipFunction_t f = nk->fn.load(std::memory_order_acquire)) return f;
+    if (nk->state.load(std::memory_order_acquire) != 2) return nullptr;
+    State& s = S();
+    std::lock_guard<std::mutex> g(s.load_mu);
+    if (nk->state.load(std::memory_order_acquire) == 2) load(s, nk);
+    return nk->fn.load(std::memory_order_acquire);
 }
 
 Stats stats() {

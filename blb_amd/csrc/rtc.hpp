@@ -13,8 +13,12 @@
 // level further: a compiled kernel per cached inverse.
 //
 // Compilation runs on a background thread by default (knob BLBRS_RTC = 1): the pass keeps the
-// table kernel until its network is loaded, so no call waits on the compiler.  BLBRS_RTC = 2
-// compiles in the calling thread on first use, 0 disables run-time networks.  A compile or
+// table kernel until its network is compiled, so no call waits on the compiler.  That thread
+// makes no HIP call: hipRTC is host-only, and the code object is loaded (hipModuleLoadData) by
+// the next launch that wants it, in the launching thread (ready()).  A background module load
+// racing the library's other threads was followed by illegal-address faults in the GPU suite
+// (DESIGN §4h), so HIP work stays on the threads that own the streams.  BLBRS_RTC = 2 compiles
+// and loads in the calling thread on first use, 0 disables run-time networks.  A compile or
 // load failure leaves the pass on tables (counted in blbrs_rtc_get_stats).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -31,7 +35,9 @@ namespace rtc {
 
 struct NetKernel {
     std::atomic<hipFunction_t> fn{nullptr};  // set once loaded
-    std::atomic<int> state{0};               // 0 pending, 1 ready, -1 failed
+    std::atomic<int> state{0};               // 0 compiling, 2 compiled (not loaded), 1 ready, -1 failed
+    std::atomic<const void*> code{nullptr};  // the compiled code object (the compile cache's; set with state 2)
+    int device = 0;                          // the device it is loaded on
     int u = 0;                               // 16-byte chunks per lane per tile
     int ops = 0;                             // VALU ops of the generated network per 8-dword group
 };
@@ -51,6 +57,10 @@ bool eligible(int k, int rows);
 // valid for the life of the process (fn == nullptr until it is ready).
 NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const uint8_t* coef);
 
+// The loaded kernel of `nk`, loading its compiled code object on nk->device in the calling thread
+// when that has not happened yet; nullptr while it compiles or after a failure.  Called per launch.
+hipFunction_t ready(NetKernel* nk);
+
 // The generated network's source for rows x k coefficients (tests, tools).
 std::string network_source(int k, int rows, const uint8_t* coef, bool cse, int* ops);
 
@@ -64,8 +74,8 @@ struct Stats {
     double compile_ms = 0;  // total compile time
 };
 Stats stats();
-// Blocks until no compile or load is queued or running, or timeout_ms passes (< 0: forever);
-// true when idle.
+// Blocks until no compile is queued or running, or timeout_ms passes (< 0: forever); true when
+// idle.  A compiled network is loaded by the next launch that wants it.
 bool wait_idle(long timeout_ms);
 // The compiler log of the first failure ("" if none).
 std::string first_failure();

@@ -433,14 +433,16 @@ int blbrs_get_tuning(const char* name, long* value);
 
 /* Decode networks generated per erasure pattern and compiled with hipRTC.
  * A wide decode pass (k + rows > BLBRS_RTC_WIDE) requests its network on first use; with
- * BLBRS_RTC = 1 (default) it compiles in the background and the pass runs the table kernel until
- * the network is loaded, with BLBRS_RTC = 2 the first call compiles it, 0 disables them. */
+ * BLBRS_RTC = 1 (default) it compiles in the background (a host-only thread, no HIP call) and the
+ * pass runs the table kernel until the network is compiled; the next launch of the pass then
+ * loads the code object in its own thread.  With BLBRS_RTC = 2 the first call compiles and loads
+ * it, 0 disables them. */
 typedef struct {
     uint64_t requested;  /* networks requested (one per pass, mode, addressing, device) */
     uint64_t compiled;   /* distinct sources compiled */
     uint64_t loaded;     /* kernels loaded on a device */
     uint64_t failed;     /* compile or load failures (those passes stay on tables) */
-    uint64_t pending;    /* queued, not yet loaded */
+    uint64_t pending;    /* queued, not yet compiled */
     double compile_ms;   /* total compile time */
 } blbrs_rtc_stats;
 int blbrs_rtc_get_stats(blbrs_rtc_stats* out);
