@@ -133,14 +133,20 @@ def cpu_baseline(k, m, seconds):
         stripes.append((data, par))
     O.code(rows, stripes[0][0], stripes[0][1], use_avx2=True, threads=threads)  # warm
     done, t0 = 0, time.perf_counter()
+    intervals, i_done, i_t0 = [], 0, t0   # ~1 s windows: a shared host's load shows up as spread
     while True:
         for data, par in stripes:
             O.code(rows, data, par, use_avx2=True, threads=threads)
         done += nstripes
-        el = time.perf_counter() - t0
+        now = time.perf_counter()
+        el = now - t0
+        if now - i_t0 >= 1.0:
+            intervals.append((done - i_done) * k * TRACT / GIB / (now - i_t0))
+            i_done, i_t0 = done, now
         if el >= seconds:
             break
     gibps = done * k * TRACT / GIB / el
+    intervals.sort()
     # Thread sweep (1.5 s per point) on the same stripes: how the rate scales with cores.
     sweep = {}
     for t in (1, 2, 4, 8, 16):
@@ -155,6 +161,8 @@ def cpu_baseline(k, m, seconds):
     out = {"value": round(gibps, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
            "per_thread_GiBps": round(gibps / threads, 3),
            "thread_sweep_GiBps": sweep,
+           "interval_GiBps": {"min": round(intervals[0], 2), "median": round(intervals[len(intervals) // 2], 2),
+                              "max": round(intervals[-1], 2), "windows": len(intervals)} if intervals else None,
            "scaling_note": "per_thread_GiBps x a host's cores is an upper bound; the sweep shows how far "
                            "from linear the rate already is at the job's share",
            "nproc": affinity, "os_cpu_count": os.cpu_count(), "omp_num_threads": omp or None,
