@@ -234,3 +234,53 @@ def test_gpu_tractserver_recovery_rpc_with_indexmap_padding(k, m, nbad, knob, or
     for j, idx in enumerate(req.index_map[k:k + nbad]):
         got = np.concatenate([b for (_, _, b, _) in t.ctl_write_calls[f"new{j}"]])
         assert np.array_equal(got, host[idx]), (k, m, bad, idx)
+
+
+@pytest.mark.gpu
+def test_gpu_network_loaded_once_by_concurrent_launches(knob):
+    """Default mode: the background thread only compiles; the first launches that find the code
+    object compiled load it in their own thread (rtc::ready).  Eight threads, each on its own
+    stream, race to that first load of one RS(12,5) pattern: exactly one module load, every
+    result bit-exact, no failure."""
+    import threading
+    torch = _torch()
+    knob("BLBRS_RTC", 1)
+    k, m = 12, 5
+    S, B = 2 * 16384 + 48, 2
+    host = _oracle_stripes(k, m, B, S, 31)
+    enc = rs.New(k, m)
+    present = rpc_present(k, m, [0, 4, 11])
+    st0 = torch.from_numpy(host).cuda()
+    enc.ReconstructBatch(st0, present)           # requests the network; runs the tables
+    assert np.array_equal(st0.cpu().numpy(), host)
+    assert rs.rtc_wait(120_000)                  # compiled, not yet loaded
+    before = rs.rtc_stats()
+    bufs = [torch.from_numpy(host).cuda() for _ in range(8)]
+    for b in bufs:
+        for i in range(k + m):
+            if not present[i]:
+                b[:, i].fill_(0x3C)
+    torch.cuda.synchronize()
+    start, errors = threading.Barrier(8), []
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                start.wait()
+                enc.ReconstructBatch(bufs[t], present)
+            s.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for b in bufs:
+        assert np.array_equal(b.cpu().numpy(), host)
+    after = rs.rtc_stats()
+    assert after["failed"] == before["failed"]
+    assert after["loaded"] - before["loaded"] == 1, (before, after)   # one pass, one device
