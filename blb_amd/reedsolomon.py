@@ -654,7 +654,8 @@ def rtc_stats() -> dict:
 
 
 def rtc_wait(timeout_ms: int = -1) -> bool:
-    """Wait for queued run-time networks to compile and load; False on timeout."""
+    """Wait for queued run-time networks to compile; False on timeout.  A compiled network is
+    loaded by the next launch of its pass, in the launching thread."""
     rc = _lib.load().blbrs_rtc_wait(int(timeout_ms))
     if rc == ErrLimit.code:
         return False
