@@ -170,17 +170,9 @@ void rs_code_kernel(CodeArgs a) {
 
     // Blocks are dealt round-robin over the 8 XCDs; with xcd_remap each XCD streams its own
     // contiguous eighth of the (stripe, tile) space instead of every 8th tile.
-    // xcd_remap 2 (a capped grid, BLBRS_CODE_GRID): each XCD's blocks loop over its own eighth.
-    uint32_t first = blockIdx.x, stride = gridDim.x, end = total;
-    if (a.xcd_remap == 1) {
-        first = (first % 8u) * (gridDim.x / 8u) + first / 8u;
-    } else if (a.xcd_remap == 2) {
-        const uint32_t region = (total + 7u) / 8u, x = blockIdx.x % 8u;
-        first = x * region + blockIdx.x / 8u;
-        stride = gridDim.x / 8u;
-        end = min(total, (x + 1u) * region);
-    }
-    for (uint32_t t = first; t < end; t += stride) {
+    uint32_t first = blockIdx.x;
+    if (a.xcd_remap) first = (first % 8u) * (gridDim.x / 8u) + first / 8u;
+    for (uint32_t t = first; t < total; t += gridDim.x) {
         const uint32_t b = t / a.tiles_per_stripe;
         const uint64_t tile_off = static_cast<uint64_t>(t - b * a.tiles_per_stripe) * kTile;
         if (!aligned || tile_off + kTile > a.S) {

@@ -138,11 +138,6 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc:
         if (total >= 64) {  // one tile per block; a multiple of 8 blocks for the XCD remap
             grid = total & ~uint64_t{7};
             a.xcd_remap = 1;
-            const long cap = tune::get(tune::kCodeGrid);   // A/B: fewer blocks, each looping over tiles
-            if (cap >= 8 && static_cast<uint64_t>(cap) < grid) {
-                grid = static_cast<uint64_t>(cap) & ~uint64_t{7};
-                a.xcd_remap = 2;
-            }
         }
         hipError_t e;
         if (rfn) {

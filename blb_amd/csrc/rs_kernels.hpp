@@ -26,8 +26,7 @@ struct CodeArgs {
     int32_t rows;             // outputs per stripe (<= kMaxRows)
     int32_t aligned;          // every shard address 16-byte aligned (vector path allowed)
     int32_t* mismatch;        // verify: [B] flags (device)
-    int32_t xcd_remap;        // set by launch_code(): 1 = block b starts at tile (b%8)*(grid/8) + b/8;
-                              // 2 = capped grid, XCD b%8 loops over its own eighth of the tiles
+    int32_t xcd_remap;        // set by launch_code(): block b starts at tile (b%8)*(grid/8) + b/8
     int32_t nstore;           // kStoreVerify: rows [0, nstore) are stored, the rest compared
     int32_t parity;           // rows = encode parity rows 0..rows-1 of k: the compiled network
                               //   (gf_bitslice.hpp) where the shape has one

@@ -20,7 +20,7 @@ constexpr Def kDefs[kCount] = {
     {"BLBRS_BITSLICE", 1}, {"BLBRS_OCC_LDS", 0},       {"BLBRS_OCC_LDS_ECT", 0}, {"BLBRS_PACK_VARIANT", -1},
     {"BLBRS_PE_CM_WIDE", 1}, {"BLBRS_HOST_ZC", -1},    {"BLBRS_EC_PERSISTENT", 0}, {"BLBRS_EC_FLAGS", 0},
     {"BLBRS_RTC", 1},      {"BLBRS_RTC_CSE", 0},       {"BLBRS_RTC_WIDE", 13},      {"BLBRS_RTC_ENCODE", 0},
-    {"BLBRS_RTC_WPE", 0},     {"BLBRS_RTC_ROW_STORES", 1}, {"BLBRS_CODE_GRID", 0},
+    {"BLBRS_RTC_WPE", 0},     {"BLBRS_RTC_ROW_STORES", 1},
 };
 
 // The environment is read once, here (thread-safe static initialisation).

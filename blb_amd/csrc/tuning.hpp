@@ -27,8 +27,6 @@ enum Knob : int {
     kRtcEncode,      // BLBRS_RTC_ENCODE: encode passes too take run-time networks instead of the compiled ones (0; A/B)
     kRtcWpe,         // BLBRS_RTC_WPE: waves per SIMD run-time networks of k + rows <= 14 ask for (0 = the compiler's choice)
     kRtcRowStores,   // BLBRS_RTC_ROW_STORES: run-time networks store each row as it is formed (1) or all rows at the end (0)
-    kCodeGrid,       // BLBRS_CODE_GRID: cap on rs_code_kernel workgroups per launch (0 = one per tile; A/B of
-                     // fewer resident waves, which loop over the tiles)
     kCount
 };
 

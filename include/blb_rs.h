@@ -425,7 +425,7 @@ int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t s
 /* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_OCC_LDS, BLBRS_OCC_LDS_ECT,
  * BLBRS_PACK_VARIANT, BLBRS_PE_CM_WIDE, BLBRS_HOST_ZC, BLBRS_EC_PERSISTENT, BLBRS_EC_FLAGS,
  * BLBRS_RTC, BLBRS_RTC_CSE, BLBRS_RTC_WIDE, BLBRS_RTC_ENCODE, BLBRS_RTC_WPE,
- * BLBRS_RTC_ROW_STORES, BLBRS_CODE_GRID; blb_amd/csrc/tuning.hpp) start from the environment, read
+ * BLBRS_RTC_ROW_STORES; blb_amd/csrc/tuning.hpp) start from the environment, read
  * once, and change only here -- never by setenv while the library runs.  INVALID_ARG for an
  * unknown name. */
 int blbrs_set_tuning(const char* name, long value);

@@ -549,27 +549,3 @@ def test_constant_data_edge_fixtures(oracle_lib, dev, k, m, fill):
         enc.Reconstruct(cur)
         assert all(np.array_equal(cur[i], sh[i]) for i in range(k + m)), (k, m, fill, S)
 
-
-@pytest.mark.parametrize("k,m", [(6, 3), (12, 5)])
-def test_capped_grid_covers_every_tile(oracle_lib, dev, knob, k, m):
-    """BLBRS_CODE_GRID (A/B: fewer workgroups, each XCD's blocks looping over its own eighth of
-    the tiles): encode, verify and a decode stay bit-exact vs the oracle for caps that do and do
-    not divide the tile count, with a ragged last tile in every stripe."""
-    rng = np.random.default_rng(7 * k + m)
-    B, S = 12, 5 * 16384 + 333          # >= 64 tiles: the cap applies (launch_code)
-    data = [rand_shards(rng, k, S) for _ in range(B)]
-    want = [oracle_encode(oracle_lib, k, m, d) for d in data]
-    host = np.stack([np.stack(d + w) for d, w in zip(data, want)])
-    enc = rs.New(k, m)
-    for cap in (8, 24, 64, 200):
-        knob("BLBRS_CODE_GRID", cap)
-        st = torch.from_numpy(host).to(dev)
-        st[:, k:].fill_(0x5A)
-        enc.EncodeBatch(st)
-        assert np.array_equal(st.cpu().numpy(), host), cap
-        assert bool(enc.VerifyBatch(st).all()), cap
-        present = [i not in (0, k + 1) for i in range(k + m)]
-        st[:, 0].fill_(0)
-        st[:, k + 1].fill_(0)
-        enc.ReconstructBatch(st, present)
-        assert np.array_equal(st.cpu().numpy(), host), (cap, "reconstruct")

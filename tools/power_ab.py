@@ -5,9 +5,11 @@ round by round; each variant runs for about --secs seconds of back-to-back launc
 GPU's metrics table is read before and after (amdsmi, read-only):
   median launch ms, PPT residency (ppt_residency_acc / accumulation_counter over the run),
   mean socket power from the energy accumulator, gfx clock samples.
-Variants are library knobs (rs.tuning): grid caps (BLBRS_CODE_GRID: fewer resident waves
-looping over the tiles), the compiled bit-plane network instead of the v_perm tables
-(BLBRS_BITSLICE=2: different VALU work for the same bytes).  Prints one JSON line per variant
+Variants are library knobs (rs.tuning): the compiled bit-plane network instead of the v_perm
+tables (BLBRS_BITSLICE=2: different VALU work for the same bytes).  The grid caps in
+profiles/r04/clocks/power_ab.jsonl used a knob (BLBRS_CODE_GRID, fewer resident waves looping
+over the tiles) of the build at commit f5141c9; it was measured 10 % slower and removed, so the
+shipped kernel stays the one validated.  Prints one JSON line per variant
 per round and a summary."""
 import argparse
 import ctypes
@@ -25,8 +27,7 @@ from blb_amd import reedsolomon as rs  # noqa: E402
 p = argparse.ArgumentParser()
 p.add_argument("--secs", type=float, default=2.0)
 p.add_argument("--rounds", type=int, default=3)
-p.add_argument("--variants", default="default:;grid2048:BLBRS_CODE_GRID=2048;grid1024:BLBRS_CODE_GRID=1024;"
-                                      "grid512:BLBRS_CODE_GRID=512;network:BLBRS_BITSLICE=2")
+p.add_argument("--variants", default="default:;network:BLBRS_BITSLICE=2")
 a = p.parse_args()
 
 variants = []
