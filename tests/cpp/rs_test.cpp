@@ -902,6 +902,79 @@ static void TestConcurrentHostSlots(T* t) {
                 (unsigned long long)l1.bytes, refused.load(), mixed_calls.load());
 }
 
+// Wide recovery from many threads at once (RS(12,5), 2..5 erasures from a small set of
+// patterns): every pass with k + rows > 13 requests a run-time network, the background thread
+// compiles it (no HIP call there), and whichever launching thread next finds it compiled loads
+// it while the others keep launching -- the interleaving rtc.hpp describes.  Shards are pool
+// buffers or pageable memory.  Every rebuilt shard is compared with the truth.
+static void TestConcurrentWideRecovery(T* t) {
+    const int k = 12, m = 5, n = k + m, threads = 8, iters = 12;
+    static const GfTable gf;
+    blbrs_encoder* enc = nullptr;
+    if (blbrs_new(k, m, &enc) != BLBRS_OK) Fatalf("New: %s", blbrs_last_error());
+    uint8_t mat[n * k];
+    blbrs_matrix(enc, mat, sizeof(mat));
+    blbrs_rtc_stats st0{};
+    blbrs_rtc_get_stats(&st0);
+    const std::vector<std::vector<int>> patterns = {{1, 3}, {0, 5, 11}, {2, 4, 6, 8}, {1, 3, 5, 8, 10}, {12, 14}, {0, 13, 16}};
+    std::mutex emu;
+    std::vector<std::string> errors;
+    auto report = [&](const std::string& s) {
+        std::lock_guard<std::mutex> g(emu);
+        if (errors.size() < 20) errors.push_back(s);
+    };
+    std::vector<std::thread> th;
+    for (int w = 0; w < threads; ++w)
+        th.emplace_back([&, w] {
+            std::mt19937_64 rng(977 + w);
+            for (int it = 0; it < iters; ++it) {
+                const size_t sizes[] = {3 * 16384 + 123, 1u << 20, 65536};
+                const size_t S = sizes[rng() % 3];
+                const bool pool = rng() % 2;
+                uint8_t* p[n];
+                bool from_pool[n];
+                for (int i = 0; i < n; ++i) {
+                    size_t cap = 0;
+                    from_pool[i] = pool && blbrs_buffer_get(S, &p[i], &cap) == BLBRS_OK;
+                    if (!from_pool[i]) p[i] = static_cast<uint8_t*>(std::malloc(S));
+                }
+                std::vector<uint8_t> truth(n * S, 0);
+                for (int i = 0; i < k; ++i)
+                    for (size_t b = 0; b < S; ++b) truth[i * S + b] = static_cast<uint8_t>(rng());
+                for (int r = k; r < n; ++r)
+                    for (int i = 0; i < k; ++i) {
+                        const uint8_t* row = gf.mul[mat[r * k + i]];
+                        for (size_t b = 0; b < S; ++b) truth[r * S + b] ^= row[truth[i * S + b]];
+                    }
+                for (int i = 0; i < n; ++i) std::memcpy(p[i], truth.data() + i * S, S);
+                const std::vector<int>& bad = patterns[(w + it) % patterns.size()];
+                std::vector<size_t> lens(n, S);
+                for (int i : bad) {
+                    lens[i] = 0;
+                    std::memset(p[i], 0xA5, S);
+                }
+                const std::string where = "thread " + std::to_string(w) + " iter " + std::to_string(it) +
+                                          " S=" + std::to_string(S);
+                if (blbrs_reconstruct(enc, p, lens.data()) != BLBRS_OK) report(where + ": " + blbrs_last_error());
+                for (int i : bad)
+                    if (std::memcmp(p[i], truth.data() + i * S, S) != 0) report(where + ": shard " + std::to_string(i));
+                for (int i = 0; i < n; ++i) {
+                    if (from_pool[i]) blbrs_buffer_put(p[i]);
+                    else std::free(p[i]);
+                }
+            }
+        });
+    for (auto& x : th) x.join();
+    blbrs_rtc_stats st1{};
+    blbrs_rtc_get_stats(&st1);
+    blbrs_free(enc);
+    for (const auto& s : errors) t->Errorf("%s", s.c_str());
+    if (st1.failed != st0.failed) t->Errorf("run-time network failures: %llu", (unsigned long long)(st1.failed - st0.failed));
+    std::printf("    run-time networks: %llu requested, %llu compiled, %llu loaded\n",
+                (unsigned long long)(st1.requested - st0.requested), (unsigned long long)(st1.compiled - st0.compiled),
+                (unsigned long long)(st1.loaded - st0.loaded));
+}
+
 int main(int argc, char** argv) {
     const bool cpu_only = argc > 1 && std::string(argv[1]) == "--cpu";
     struct Test { const char* name; void (*fn)(T*); bool gpu; };
@@ -927,6 +1000,7 @@ int main(int argc, char** argv) {
         {"TestRSEncodeConcurrentBatched", TestRSEncodeConcurrentBatched, true},
         {"TestRecoveryWriteCRC", TestRecoveryWriteCRC, true},
         {"TestConcurrentHostSlots", TestConcurrentHostSlots, true},
+        {"TestConcurrentWideRecovery", TestConcurrentWideRecovery, true},
     };
     int failed = 0, ran = 0;
     for (const Test& tc : tests) {

@@ -7,14 +7,15 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/tools/_build/tsan
 mkdir -p "$OUT"
 pids=()
-for f in runtime rs_kernels crc32c encode_crc encode_crc_tile pack pack_encode blbrs; do
+make -C "$ROOT/blb_amd" _build/rtc_headers.inc >/dev/null   # the device headers rtc.hip embeds
+for f in tuning runtime rtc rs_kernels crc32c encode_crc encode_crc_tile pack pack_encode blbrs; do
   /opt/rocm/bin/hipcc -O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Xarch_host -fsanitize=thread \
-    -c "$ROOT/blb_amd/csrc/$f.hip" -o "$OUT/$f.o" &
+    -I"$ROOT/blb_amd/_build" -c "$ROOT/blb_amd/csrc/$f.hip" -o "$OUT/$f.o" &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -fno-gpu-sanitize -fsanitize=thread \
-  -o "$OUT/libblbrs.so" "$OUT"/*.o
+  -o "$OUT/libblbrs.so" "$OUT"/*.o -lhiprtc
 rm -f "$OUT"/*.o
 /opt/rocm/llvm/bin/clang++ -O1 -g -std=c++17 -pthread -fsanitize=thread -o "$OUT/rs_test_tsan" \
   "$ROOT/tests/cpp/rs_test.cpp" "$ROOT"/blb_amd/host/{reedsolomon,tractserver,client}.cpp \
