@@ -549,3 +549,33 @@ def test_constant_data_edge_fixtures(oracle_lib, dev, k, m, fill):
         enc.Reconstruct(cur)
         assert all(np.array_equal(cur[i], sh[i]) for i in range(k + m)), (k, m, fill, S)
 
+
+
+@pytest.mark.parametrize("k,m", [(250, 6), (200, 56), (1, 255), (128, 128)])
+def test_maximum_shard_counts_vs_oracle(oracle_lib, dev, k, m):
+    """k + m = 256 (klauspost's limit, ErrMaxShardNum above it): encode of host shards and of a
+    device batch against the oracle, then Reconstruct / ReconstructData with all m slots lost
+    (m above the kernel's 8 rows per pass: the plan splits the rows into passes)."""
+    rng = np.random.default_rng(k * 3 + m)
+    enc = rs.New(k, m)
+    for S in (1, 4099):
+        data = rand_shards(rng, k, S)
+        want = oracle_encode(oracle_lib, k, m, data)
+        sh = [d.copy() for d in data] + [np.full(S, 0x11, np.uint8) for _ in range(m)]
+        enc.Encode(sh)
+        assert all(np.array_equal(sh[k + j], want[j]) for j in range(m)), (k, m, S)
+        st = torch.from_numpy(np.stack(data + want)[None]).to(dev)
+        st[:, k:].fill_(0x5A)
+        enc.EncodeBatch(st)
+        assert np.array_equal(st[0].cpu().numpy(), np.stack(data + want)), (k, m, S, "batch")
+        full = data + want
+        lost = sorted(rng.choice(k + m, m, replace=False).tolist())
+        for data_only in (False, True):
+            cur = [None if i in lost else full[i].copy() for i in range(k + m)]
+            (enc.ReconstructData if data_only else enc.Reconstruct)(cur)
+            ref = oracle_lib.reconstruct(k, m, [None if i in lost else full[i] for i in range(k + m)], data_only)
+            for i in range(k + m):
+                if ref[i] is None:
+                    assert cur[i] is None, (k, m, i)
+                else:
+                    assert np.array_equal(cur[i], ref[i]) and np.array_equal(cur[i], full[i]), (k, m, lost, i)
