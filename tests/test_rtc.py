@@ -284,3 +284,35 @@ def test_gpu_network_loaded_once_by_concurrent_launches(knob):
     after = rs.rtc_stats()
     assert after["failed"] == before["failed"]
     assert after["loaded"] - before["loaded"] == 1, (before, after)   # one pass, one device
+
+
+@pytest.mark.gpu
+def test_gpu_network_pointer_table_misaligned_and_ragged(knob):
+    """A wide decode through the device pointer table (blbrs_reconstruct_dev_ptrs) on its
+    run-time network, with one input shard 1 byte off 16-byte alignment and shard lengths that
+    end mid-tile: the launch takes the table path for unaligned / partial tiles (rs_code.hpp),
+    so every byte must still be the oracle's."""
+    torch = _torch()
+    knob("BLBRS_RTC", 2)
+    k, m = 12, 5
+    enc = rs.New(k, m)
+    for S, odd in ((3 * 8192 + 4, 2), (4 * 8192, None), (8192 * 2 + 777, 0)):
+        host = _oracle_stripes(k, m, 1, S, S)[0]
+        bad = [1, 3, 5, 8, 10]
+        present = rpc_present(k, m, bad)
+        shards = []
+        for i in range(k + m):
+            if not present[i]:
+                shards.append(torch.empty(0, dtype=torch.uint8, device="cuda"))
+            elif i == odd:
+                t = torch.empty(S + 1, dtype=torch.uint8, device="cuda")[1:]
+                t.copy_(torch.from_numpy(host[i]))
+                shards.append(t)
+            else:
+                shards.append(torch.from_numpy(host[i]).cuda())
+        before = rs.rtc_stats()
+        enc.Reconstruct(shards)
+        torch.cuda.synchronize()
+        for i in range(k + m):
+            assert np.array_equal(shards[i].cpu().numpy(), host[i]), (S, odd, i)
+        assert rs.rtc_stats()["failed"] == before["failed"]
