@@ -15,6 +15,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "gf256.hpp"
 #include "tuning.hpp"
 
@@ -165,11 +167,14 @@ struct Job {
 struct State {
     std::mutex mu;
     std::condition_variable cv_idle;
+    std::condition_variable cv_work;  // the worker waits here for jobs (or exit)
     std::map<std::string, std::unique_ptr<NetKernel>> kernels;        // device|source
     std::map<std::string, std::shared_ptr<Compiled>> compiled;        // source
     std::deque<Job> queue;
-    std::mutex load_mu;   // module loads (ready()), one at a time
-    bool worker = false;
+    // Started by the first queued job, joined at exit.  Owned by the process that started it: a
+    // fork()ed child inherits the object but not the thread, so it starts (and joins) its own.
+    std::thread* worker = nullptr;
+    pid_t worker_pid = 0;
     int busy = 0;
     bool exiting = false;
     Stats st;
@@ -188,8 +193,20 @@ void note_failure(State& s, const std::string& what) {
     }
 }
 
-// Compile (outside the lock); nullptr + log on failure.
+void exit_hook_again();
+
+// Everything this module does through comgr (LLVM in this process) -- a hipRTC compile, a
+// hipModuleLoadData -- holds this lock, so no two of them overlap: compiles on the worker and
+// module loads on launching threads did overlap, and such runs ended in LLVM errors inside
+// hiprtcCompileProgram and heap corruption (tools/comgr_race.py).
+std::mutex& comgr_mu() {
+    static std::mutex* m = new std::mutex;
+    return *m;
+}
+
+// Compile (outside the state lock); nullptr + log on failure.
 std::shared_ptr<Compiled> compile(const std::string& src, const std::string& name_expr, std::string* log) {
+    std::lock_guard<std::mutex> comgr(comgr_mu());
     std::vector<const char*> names, srcs;
     for (const Header& h : kHeaders) {
         names.push_back(h.name);
@@ -226,6 +243,7 @@ std::shared_ptr<Compiled> compile(const std::string& src, const std::string& nam
         }
     }
     hiprtcDestroyProgram(&prog);
+    exit_hook_again();
     return out;
 }
 
@@ -256,7 +274,7 @@ void run_job(State& s, const Job& j) {
     j.nk->state.store(2, std::memory_order_release);
 }
 
-// Load a compiled code object on nk->device in this thread (s.load_mu held).
+// Load a compiled code object on nk->device in this thread (comgr_mu held).
 void load(State& s, NetKernel* nk) {
     const Compiled* c = static_cast<const Compiled*>(nk->code.load(std::memory_order_acquire));
     int prev = 0;
@@ -267,6 +285,7 @@ void load(State& s, NetKernel* nk) {
     if (e == hipSuccess) e = hipModuleLoadData(&mod, c->code.data());
     if (e == hipSuccess) e = hipModuleGetFunction(&fn, mod, c->lowered.c_str());
     (void)hipSetDevice(prev);
+    exit_hook_again();
     std::lock_guard<std::mutex> g(s.mu);
     if (e != hipSuccess || !fn) {
         (void)hipGetLastError();
@@ -279,10 +298,15 @@ void load(State& s, NetKernel* nk) {
     nk->state.store(1, std::memory_order_release);
 }
 
+// One compiler thread for the life of the process: it sleeps on cv_work while idle and ends
+// only at exit, where at_exit joins it, so its thread-local teardown (LLVM's, inside hipRTC) is
+// over before the process's static destructors run.
 void worker_loop() {
     State& s = S();
     std::unique_lock<std::mutex> lk(s.mu);
-    while (!s.queue.empty() && !s.exiting) {
+    for (;;) {
+        s.cv_work.wait(lk, [&] { return s.exiting || !s.queue.empty(); });
+        if (s.exiting) break;
         Job j = std::move(s.queue.front());
         s.queue.pop_front();
         ++s.busy;
@@ -291,20 +315,55 @@ void worker_loop() {
         lk.lock();
         --s.busy;
         if (s.st.pending) --s.st.pending;
+        if (s.queue.empty()) s.cv_idle.notify_all();
     }
-    s.worker = false;
     s.cv_idle.notify_all();
 }
 
-// At exit: stop taking jobs and let a running compile finish before HIP tears down (this handler
-// is registered after HIP initialised, so it runs first).
+// At exit: stop taking jobs and let a running compile finish before the compiler is torn down.
+// hipRTC runs LLVM (comgr) in this process, and comgr's static destructors run at exit in
+// reverse order of registration: a compile still running on the worker when they run aborts the
+// process (seen: "LLVM ERROR: Cannot implicitly convert a scalable size ...", and a corrupted
+// heap, at the exit of a program whose last calls had queued networks).  So the handler is
+// registered after comgr is loaded (exit_hook), again after every compile and module load
+// (LLVM's lazily built statics), and it runs before either set of destructors.  It joins the worker
+// rather than waiting for a flag, so the thread's own teardown (LLVM thread-locals) is also
+// finished before them: a detached worker that ended as exit began crashed there (segfault at
+// the exit of tests/cpp/rs_test, 1 run in 2).
 void at_exit() {
     State& s = S();
     std::unique_lock<std::mutex> lk(s.mu);
     s.exiting = true;
     s.st.pending -= std::min<uint64_t>(s.st.pending, s.queue.size());
     s.queue.clear();
-    s.cv_idle.wait_for(lk, std::chrono::seconds(60), [&] { return !s.worker; });
+    s.cv_work.notify_all();
+    lk.unlock();
+    // Only the library's own worker is waited for: its code after the compile is this file's.
+    // A caller thread compiling (BLBRS_RTC = 2, blbrs_rtc_compile) returns into its caller, whose
+    // runtime may already be gone (a Python daemon thread crashes there), so it is not held.
+    if (s.worker && s.worker_pid == getpid() && s.worker->joinable() &&
+        s.worker->get_id() != std::this_thread::get_id())
+        s.worker->join();
+}
+
+// Loads comgr (hiprtcCreateProgram does; no compile) and then registers at_exit, once.  Called
+// before the first compile of the process, without s.mu held.
+void exit_hook() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        std::lock_guard<std::mutex> comgr(comgr_mu());
+        hiprtcProgram p = nullptr;
+        if (hiprtcCreateProgram(&p, "", "blbrs_load.hip", 0, nullptr, nullptr) == HIPRTC_SUCCESS)
+            hiprtcDestroyProgram(&p);
+        std::atexit(at_exit);
+    });
+}
+
+// After every compile and module load: once more, behind whatever statics comgr / LLVM built
+// lazily on the way (their destructors then run after at_exit).  Bounded; at_exit is idempotent.
+void exit_hook_again() {
+    static std::atomic<int> n{0};
+    if (n.fetch_add(1, std::memory_order_relaxed) < 4096) std::atexit(at_exit);
 }
 
 std::string kernel_source(int k, int rows, const uint8_t* coef, bool cse, int* ops) {
@@ -354,12 +413,17 @@ bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef,
     int u = 0, ops = 0;
     unit(k, rows, mode, strided, coef, &src, &name, &u, &ops);
     State& s = S();
+    exit_hook();
     {
         std::lock_guard<std::mutex> g(s.mu);
         auto it = s.compiled.find(src);
         if (it != s.compiled.end()) {
             if (code) *code = it->second->code;
             return true;
+        }
+        if (s.exiting) {
+            *log = "process exiting";
+            return false;
         }
     }
     const auto t0 = std::chrono::steady_clock::now();
@@ -381,6 +445,7 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
     unit(k, rows, mode, strided, coef, &src, &name, &u, &ops);
     const std::string key = std::to_string(device) + "|" + src;
     State& s = S();
+    exit_hook();
     NetKernel* nk = nullptr;
     bool sync = false;
     {
@@ -399,11 +464,11 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
         if (!sync) {
             s.queue.push_back(Job{src, name, device, nk});
             ++s.st.pending;
-            if (!s.worker) {
-                static std::once_flag once;
-                std::call_once(once, [] { std::atexit(at_exit); });
-                s.worker = true;
-                std::thread(worker_loop).detach();
+            if (!s.worker || s.worker_pid != getpid()) {
+                s.worker = new std::thread(worker_loop);  // never deleted: see State
+                s.worker_pid = getpid();
+            } else {
+                s.cv_work.notify_one();
             }
         } else {
             ++s.busy;
@@ -411,7 +476,7 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
     }
     if (sync) {
         run_job(s, Job{src, name, device, nk});
-        (void)ready(nk);
+        (void)ready(nk, /*wait=*/true);
         std::lock_guard<std::mutex> g(s.mu);
         --s.busy;
         s.cv_idle.notify_all();
@@ -419,12 +484,15 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
     return nk;
 }
 
-hipFunction_t ready(NetKernel* nk) {
+hipFunction_t ready(NetKernel* nk, bool wait) {
     if (!nk) return nullptr;
     if (hipFunction_t f = nk->fn.load(std::memory_order_acquire)) return f;
     if (nk->state.load(std::memory_order_acquire) != 2) return nullptr;
     State& s = S();
-    std::lock_guard<std::mutex> g(s.load_mu);
+    // A launch does not wait for a compile in progress: the tables serve it, a later launch loads.
+    std::unique_lock<std::mutex> comgr(comgr_mu(), std::defer_lock);
+    if (wait) comgr.lock();
+    else if (!comgr.try_lock()) return nullptr;
     if (nk->state.load(std::memory_order_acquire) == 2) load(s, nk);
     return nk->fn.load(std::memory_order_acquire);
 }
@@ -438,7 +506,7 @@ Stats stats() {
 bool wait_idle(long timeout_ms) {
     State& s = S();
     std::unique_lock<std::mutex> lk(s.mu);
-    auto idle = [&] { return s.queue.empty() && !s.worker && s.busy == 0; };
+    auto idle = [&] { return s.queue.empty() && s.busy == 0; };
     if (timeout_ms < 0) {
         s.cv_idle.wait(lk, idle);
         return true;

@@ -59,7 +59,8 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
 
 // The loaded kernel of `nk`, loading its compiled code object on nk->device in the calling thread
 // when that has not happened yet; nullptr while it compiles or after a failure.  Called per launch.
-hipFunction_t ready(NetKernel* nk);
+// wait = false (launches): nullptr instead of waiting while another compile or load holds comgr.
+hipFunction_t ready(NetKernel* nk, bool wait = false);
 
 // The generated network's source for rows x k coefficients (tests, tools).
 std::string network_source(int k, int rows, const uint8_t* coef, bool cse, int* ops);

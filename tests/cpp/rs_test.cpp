@@ -12,8 +12,12 @@
 // internal/testblb/test_rs_recovery.go's reads after a tractserver dies.
 //
 // usage: rs_test [--cpu]   (--cpu: only the tests that need no GPU)
+#include <execinfo.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <csignal>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -975,7 +979,23 @@ static void TestConcurrentWideRecovery(T* t) {
                 (unsigned long long)(st1.loaded - st0.loaded));
 }
 
+// A crash (also one at exit, after the last test) prints the faulting thread's stack: frames in
+// the library are "libblbrs.so(+offset)", resolved with addr2line against the same build.
+static void crash_handler(int sig) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "rs_test: fatal signal, backtrace:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    std::signal(sig, SIG_DFL);
+    std::raise(sig);
+}
+
 int main(int argc, char** argv) {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);  // each test's line survives an abort
+    std::signal(SIGSEGV, crash_handler);
+    std::signal(SIGABRT, crash_handler);
+    std::signal(SIGBUS, crash_handler);
     const bool cpu_only = argc > 1 && std::string(argv[1]) == "--cpu";
     struct Test { const char* name; void (*fn)(T*); bool gpu; };
     const Test tests[] = {

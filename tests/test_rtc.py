@@ -14,6 +14,7 @@ GPU: every class at 1..m erasures in the RPC and client shapes, through the devi
 (strided) and the host call (pointer table) and the tractserver mirror with the curator's
 indexMap (-1 padding), bit-exact against the oracle, with the network actually loaded.
 """
+import os
 import re
 
 import numpy as np
@@ -316,3 +317,37 @@ def test_gpu_network_pointer_table_misaligned_and_ragged(knob):
         for i in range(k + m):
             assert np.array_equal(shards[i].cpu().numpy(), host[i]), (S, odd, i)
         assert rs.rtc_stats()["failed"] == before["failed"]
+
+
+_EXIT_SCRIPT = r'''
+import ctypes, sys, threading, time
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from blb_amd import _lib
+lib = _lib.load()
+rng = np.random.default_rng(int(sys.argv[2]))
+def loop():
+    while True:
+        coef = rng.integers(1, 256, 12 * 5, dtype=np.uint8)
+        n = ctypes.c_size_t(0)
+        lib.blbrs_rtc_compile(12, 5, coef.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 0, 1, None, 0,
+                              ctypes.byref(n))
+threading.Thread(target=loop, daemon=True).start()
+time.sleep(0.6)
+print("exiting", flush=True)
+'''
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_exit_with_a_compile_in_flight(seed):
+    """The library's exit handler (rtc.hip at_exit) waits for its own background compiler only:
+    a process that exits while one of ITS threads is inside hipRTC (here a Python daemon thread
+    in blbrs_rtc_compile) exits cleanly, neither hanging on that compile nor crashing when the
+    thread would return into a finalized interpreter."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _EXIT_SCRIPT, root, str(seed)], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, (p.returncode, p.stdout[-500:], p.stderr[-2000:])
+    assert "exiting" in p.stdout
