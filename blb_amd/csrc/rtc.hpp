@@ -17,9 +17,12 @@
 // makes no HIP call: hipRTC is host-only, and the code object is loaded (hipModuleLoadData) by
 // the next launch that wants it, in the launching thread (ready()).  A background module load
 // racing the library's other threads was followed by illegal-address faults in the GPU suite
-// (DESIGN §4h), so HIP work stays on the threads that own the streams.  BLBRS_RTC = 2 compiles
-// and loads in the calling thread on first use, 0 disables run-time networks.  A compile or
-// load failure leaves the pass on tables (counted in blbrs_rtc_get_stats).
+// (DESIGN §4h), so HIP work stays on the threads that own the streams.  Compiles and loads
+// share one lock (comgr, i.e. LLVM, runs in this process), a launch never waits for it, and the
+// compiler thread lives for the whole process and is joined at exit, before comgr's static
+// destructors run.  BLBRS_RTC = 2 compiles and loads in the calling thread on first use, 0
+// disables run-time networks.  A compile or load failure leaves the pass on tables (counted in
+// blbrs_rtc_get_stats).
 #pragma once
 #include <hip/hip_runtime.h>
 
