@@ -458,8 +458,9 @@ def recovery_extras(S, dev, reps=3):
       first k good replies, ReconstructData of the r missing data slots (r = 1: every other
       data piece answered; r = m: the parity pieces answered first).
 
-    Each row: the shipped path's HIP-event time (a run-time decode network where it applies,
-    DESIGN §4h, else the v_perm tables), the tables alone, algorithmic bytes B*(k+rows)*S and
+    Each row: the shipped path's HIP-event time (the v_perm tables: run-time decode networks are
+    off by default since round 5), on wide passes the opt-in network's time
+    (BLBRS_RTC), algorithmic bytes B*(k+rows)*S and
     the fraction of 8 TB/s, and the trivial-XOR stream of the same reads and writes in the same
     layout and launch shape (tools/stream_probe.hip) at the kernel's U and at its best U."""
     probe = _stream_probe()
@@ -487,16 +488,20 @@ def recovery_extras(S, dev, reps=3):
             ref = {i: st[:, i].clone() for i in targets if i < k}
             for i in targets:
                 st[:, i].fill_(0xA5)
-            e.ReconstructBatch(st, present, data_only=data_only)  # requests the network
+            with rs.tuning(BLBRS_RTC=1):
+                net = rs.rtc_eligible(k, nrows)   # a wide pass: time its opt-in run-time network too
+            with rs.tuning(BLBRS_RTC=2 if net else 0):
+                e.ReconstructBatch(st, present, data_only=data_only)  # compiles and loads the network
             torch.cuda.synchronize(dev)
             exact = all(bool(torch.equal(st[:, i], r)) for i, r in ref.items())
             if not data_only:
                 exact = exact and bool(e.VerifyBatch(st).all())
             del ref
-            rs.rtc_wait()
             u = 4 if k + nrows <= 9 else 2
-            fns = {"shipped": lambda: e.ReconstructBatch(st, present, data_only=data_only),
-                   "tables": lambda: e.ReconstructBatch(st, present, data_only=data_only)}
+            run = lambda: e.ReconstructBatch(st, present, data_only=data_only)  # noqa: E731
+            fns = {"shipped": run}
+            if net:
+                fns["network"] = run
             if probe is not None:
                 for pu in (1, 2, 4):
                     fns[f"probe_u{pu}"] = (lambda pu=pu: probe.stream_probe(
@@ -504,14 +509,16 @@ def recovery_extras(S, dev, reps=3):
             times = {key: [] for key in fns}
             for _ in range(reps):
                 for key, fn in fns.items():
-                    with rs.tuning(**({"BLBRS_RTC": 0} if key == "tables" else {})):
+                    with rs.tuning(**({"BLBRS_RTC": 2} if key == "network" else {})):
                         times[key].append(_ev_ms(fn, 1, stream, dev))
             e.EncodeBatch(st)  # the probe wrote garbage over parity shards [k, k + rows): restore them
             ms = {key: sorted(v)[len(v) // 2] for key, v in times.items()}
             nbytes = B * (k + nrows) * S
             row = {"rows": nrows, "present": [i for i in range(n) if present[i]], "algorithmic_bytes": nbytes,
                    "ms": round(ms["shipped"], 3), "frac_of_8TBps": round(nbytes / (ms["shipped"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                   "tables_ms": round(ms["tables"], 3), "network": rs.rtc_eligible(k, nrows), "bit_exact": exact}
+                   "bit_exact": exact}
+            if net:  # opt-in (BLBRS_RTC=1/2); the shipped default runs the tables
+                row["network_ms"] = round(ms["network"], 3)
             if probe is not None:
                 best = min(ms[f"probe_u{pu}"] for pu in (1, 2, 4))
                 row.update({"probe_ms_same_u": round(ms[f"probe_u{u}"], 3), "probe_ms_best_u": round(best, 3),

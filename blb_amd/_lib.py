@@ -68,6 +68,8 @@ SIGNATURES = {
     "blbrs_set_worker_limit": (_I, [_I]),
     "blbrs_get_device_stats": (_I, [_I, _P]),
     "blbrs_trim": (_I, []),
+    "blbrs_table_fault_take": (_I, [_I, _P, ctypes.POINTER(_I)]),
+    "blbrs_debug_corrupt_next_table": (_I, [_I]),
     "blbrs_set_device": (_I, [_I]),
     "blbrs_device_count": (_I, [ctypes.POINTER(_I)]),
     "blbrs_device_numa_node": (_I, [_I, ctypes.POINTER(_I)]),
@@ -79,7 +81,7 @@ SIGNATURES = {
     "blbrs_rtc_get_stats": (_I, [_P]),
     "blbrs_rtc_compile": (_I, [_I, _I, _P, _I, _I, _P, _SZ, ctypes.POINTER(_SZ)]),
     "blbrs_rtc_wait": (_I, [ctypes.c_long]),
-    "blbrs_rtc_network_source": (_I, [_I, _I, _P, _I, _P, _SZ, ctypes.POINTER(_I)]),
+    "blbrs_rtc_network_source": (_I, [_I, _I, _P, _P, _SZ, ctypes.POINTER(_I)]),
     "blbrs_last_error": (ctypes.c_char_p, []),
     "blbrs_version": (ctypes.c_char_p, []),
     "blbrs_strerror": (ctypes.c_char_p, [_I]),
@@ -111,6 +113,12 @@ class RtcStats(ctypes.Structure):
     """blbrs_rtc_stats"""
     _fields_ = [("requested", ctypes.c_uint64), ("compiled", ctypes.c_uint64), ("loaded", ctypes.c_uint64),
                 ("failed", ctypes.c_uint64), ("pending", ctypes.c_uint64), ("compile_ms", ctypes.c_double)]
+
+
+class TableFault(ctypes.Structure):
+    """blbrs_table_fault"""
+    _fields_ = [("stripe", ctypes.c_uint32), ("slot", ctypes.c_uint32), ("launch_tag", ctypes.c_uint32),
+                ("entry_tag", ctypes.c_uint32), ("address", ctypes.c_uint64)]
 
 
 class DevPart(ctypes.Structure):

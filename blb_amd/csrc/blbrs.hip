@@ -355,6 +355,8 @@ struct Stripes {
     const uint64_t* ptrs = nullptr;  // device pointer table form
     uint32_t nshards = 0;
     bool aligned = false;
+    uint32_t tag = 0;                // the table's tag (rt::tag_entries)
+    uint32_t* fault = nullptr;       //   and the record its launches report a wrong entry to
 };
 
 // Launch every pass of `plan` over `batch` stripes.
@@ -379,6 +381,8 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         a.aligned = st.aligned ? 1 : 0;
         a.mismatch = mismatch;
         a.parity = ps.parity ? 1 : 0;
+        a.ptr_tag = st.tag;
+        a.fault = st.fault;
         Mode m = mode;
         if (mode == Mode::kStoreVerify) {  // per pass: all stored, all compared, or mixed
             a.nstore = ps.nstore;
@@ -388,17 +392,13 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         // outside the compiled list) take a network generated for their coefficients once it is
         // loaded; until then, and on failure, the table kernel.
         rtc::NetKernel* net = nullptr;
-        const bool aot = bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode) &&  // compiled encode network
-                         tune::get(tune::kRtcEncode) == 0;
+        const bool aot = bs::use(ps.parity, ps.k_in, ps.rows, bs::kWideCode);  // compiled encode network
         if (!aot && bs::mode() != 0 && rtc::eligible(ps.k_in, ps.rows)) {
-            const int mi = static_cast<int>(m), ai = st.base ? 0 : 1;
-            auto& slot = ps.net->k[mi][ai];
-            const unsigned gen = tune::generation();  // knobs (BLBRS_RTC_CSE, _WPE) shape the source
+            auto& slot = ps.net->k[static_cast<int>(m)][st.base ? 0 : 1];
             rtc::NetKernel* nk = slot.load(std::memory_order_acquire);
-            if (!nk || ps.net->gen[mi][ai].load(std::memory_order_acquire) != gen) {
+            if (!nk) {
                 nk = rtc::request(plan.device, ps.k_in, ps.rows, m, st.base != nullptr, ps.coef.data());
                 slot.store(nk, std::memory_order_release);
-                ps.net->gen[mi][ai].store(gen, std::memory_order_release);
             }
             net = nk;
         }
@@ -516,7 +516,8 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         // Everything in place: one launch per step over the whole batch.
         Stripes st;
         st.nshards = n;
-        if ((rc = w->upload_table(view.data(), view.size(), &st.ptrs, &st.aligned))) return drain(rc);
+        st.fault = w->fault;
+        if ((rc = w->upload_table(view.data(), view.size(), &st.ptrs, &st.aligned, &st.tag))) return drain(rc);
         hipError_t e = hipSuccess;
         if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
         if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
@@ -527,6 +528,7 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         const hipError_t f = hipStreamSynchronize(w->s[0]);
         if (e == hipSuccess) e = f;
         if (e != hipSuccess) return drain(hip_fail(e, "zero-copy call"));
+        if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
         if (ok) *ok = flag ? 0 : 1;
         return BLBRS_OK;
     }
@@ -558,7 +560,8 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         }
     const uint64_t* tab_dev = nullptr;
     bool tab_aligned = false;
-    if ((rc = w->upload_table(table.data(), table.size(), &tab_dev, &tab_aligned))) return drain(rc);
+    uint32_t tab_tag = 0;
+    if ((rc = w->upload_table(table.data(), table.size(), &tab_dev, &tab_aligned, &tab_tag))) return drain(rc);
     hipEvent_t ev = nullptr;
     struct EvFree {
         hipEvent_t& e;
@@ -593,6 +596,8 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             st.ptrs = tab_dev + u * n;
             st.nshards = n;
             st.aligned = tab_aligned;
+            st.tag = tab_tag;
+            st.fault = w->fault;
             for (size_t t = 0; t < steps.size(); ++t)
                 if ((rc = run_plan(*plans[t], st, 1, len, steps[t].mode, w->flag, s))) return drain(rc);
             for (int i = 0, r = 0; i < n && e == hipSuccess; ++i) {
@@ -614,6 +619,7 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     const hipError_t f1 = hipStreamSynchronize(w->s[1]);
     if (e == hipSuccess) e = f0 != hipSuccess ? f0 : f1;
     if (e != hipSuccess) return drain(hip_fail(e, "staged call"));
+    if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
     if (ok) *ok = flag ? 0 : 1;
     return BLBRS_OK;
 }
@@ -710,6 +716,7 @@ struct blbrs_batcher {
         int32_t* flags_host = nullptr;  // per-stripe Verify mismatch flags
         int32_t* flags_dev = nullptr;
         size_t flags_cap = 0;
+        uint32_t* fault = nullptr;      // pinned record of the lane's table checks
         std::thread th;
     };
     size_t max_batch = 64;
@@ -752,7 +759,7 @@ struct blbrs_batcher {
         }
     }
 
-    int upload(Lane* lane, const std::vector<uint64_t>& table, const uint64_t** dev_out, bool* aligned) {
+    int upload(Lane* lane, const std::vector<uint64_t>& table, const uint64_t** dev_out, bool* aligned, uint32_t* tag) {
         if (table.size() > lane->tab_cap) {
             if (lane->tab_host) (void)hipHostFree(lane->tab_host);
             if (lane->tab_dev) (void)hipFree(lane->tab_dev);
@@ -764,14 +771,10 @@ struct blbrs_batcher {
             HIP_TRY(hipMalloc(reinterpret_cast<void**>(&lane->tab_dev), cap * 8));
             lane->tab_cap = cap;
         }
-        bool al = true;
-        for (size_t i = 0; i < table.size(); ++i) {
-            lane->tab_host[i] = table[i];
-            al = al && aligned16(table[i]);
-        }
+        *tag = rt::next_table_tag();
+        if (int rc = rt::tag_entries(table.data(), table.size(), *tag, lane->tab_host, aligned)) return rc;
         HIP_TRY(hipMemcpyAsync(lane->tab_dev, lane->tab_host, table.size() * 8, hipMemcpyHostToDevice, lane->stream));
         *dev_out = lane->tab_dev;
-        *aligned = al;
         return BLBRS_OK;
     }
 
@@ -817,7 +820,8 @@ struct blbrs_batcher {
                     std::copy(reqs[j]->views.begin(), reqs[j]->views.end(), table.begin() + j * n);
                 Stripes st;
                 st.nshards = static_cast<uint32_t>(n);
-                rc = upload(lane, table, &st.ptrs, &st.aligned);
+                st.fault = lane->fault;
+                rc = upload(lane, table, &st.ptrs, &st.aligned, &st.tag);
                 if (rc == BLBRS_OK && plan && r0.mixed) {
                     rc = flags(lane, reqs.size());
                     if (rc == BLBRS_OK)
@@ -844,6 +848,7 @@ struct blbrs_batcher {
                 // The table is rewritten by the next group: wait for this one's launches.
                 const hipError_t e = hipStreamSynchronize(lane->stream);
                 if (rc == BLBRS_OK && e != hipSuccess) rc = hip_fail(e, "batched call");
+                if (rc == BLBRS_OK) rc = rt::check_fault(lane->fault, "batched call");
             }
             for (size_t j = 0; j < reqs.size(); ++j) {
                 BatchReq* r = reqs[j];
@@ -891,6 +896,7 @@ struct blbrs_batcher {
             if (l->tab_dev) (void)hipFree(l->tab_dev);
             if (l->flags_host) (void)hipHostFree(l->flags_host);
             if (l->flags_dev) (void)hipFree(l->flags_dev);
+            if (l->fault) (void)hipHostFree(l->fault);
         }
     }
 };
@@ -996,6 +1002,7 @@ int make_batcher(int max_batch, int window_us, std::vector<int> devs, blbrs_batc
             int rc = guard.enter(d);
             hipError_t e = hipSuccess;
             if (rc == BLBRS_OK) e = hipStreamCreateWithFlags(&lane->stream, hipStreamNonBlocking);
+            if (rc == BLBRS_OK && e == hipSuccess) rc = rt::alloc_fault_record(&lane->fault);
             if (rc != BLBRS_OK || e != hipSuccess) {
                 b->shutdown();
                 delete b;
@@ -1157,10 +1164,10 @@ int blbrs_rtc_wait(long timeout_ms) {
     return rtc::wait_idle(timeout_ms) ? BLBRS_OK : fail(BLBRS_ERR_LIMIT, "run-time networks still compiling");
 }
 
-int blbrs_rtc_network_source(int k, int rows, const uint8_t* coef, int cse, char* out, size_t cap, int* ops) {
+int blbrs_rtc_network_source(int k, int rows, const uint8_t* coef, char* out, size_t cap, int* ops) {
     if (k < 1 || rows < 1 || k > 256 || rows > 256 || !coef || !out) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
     int n = 0;
-    const std::string src = rtc::network_source(k, rows, coef, cse != 0, &n);
+    const std::string src = rtc::network_source(k, rows, coef, &n);
     if (src.size() + 1 > cap) return fail(BLBRS_ERR_INVALID_ARG, "buffer too small");
     std::memcpy(out, src.c_str(), src.size() + 1);
     if (ops) *ops = n;
@@ -1309,14 +1316,18 @@ int blbrs_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_stride, 
     return dev_run(enc, dc.dev, "E", *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
 }
 
-static int upload_ptrs(uint8_t* const* ptrs, size_t count, hipStream_t stream, rt::PtrLease& lease,
-                       const uint64_t** dev_out, bool* aligned) {
+// A caller's device pointer table, tagged; its launches report to the device's record (the call
+// is asynchronous: blbrs_table_fault_take reads it once the caller's stream has run).
+static int upload_ptrs(uint8_t* const* ptrs, size_t count, hipStream_t stream, rt::PtrLease& lease, int dev,
+                       Stripes* st) {
     std::vector<uint64_t> v(count);
     for (size_t i = 0; i < count; ++i) {
         if (!ptrs[i]) return fail(BLBRS_ERR_INVALID_ARG, "NULL shard pointer");
         v[i] = reinterpret_cast<uint64_t>(ptrs[i]);
     }
-    return lease.upload(v.data(), count, stream, dev_out, aligned);
+    st->fault = rt::device_fault_record(dev);
+    if (!st->fault) return fail(BLBRS_ERR_HIP, "no fault record for device " + std::to_string(dev));
+    return lease.upload(v.data(), count, stream, &st->ptrs, &st->aligned, &st->tag);
 }
 
 int blbrs_encode_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
@@ -1329,7 +1340,7 @@ int blbrs_encode_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t
     if (rc) return rc;
     rt::PtrLease lease;
     Stripes st;
-    if ((rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, &st.ptrs, &st.aligned)))
+    if ((rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, dc.dev, &st)))
         return rc;
     st.nshards = n;
     auto hp = enc->encode_plan();
@@ -1381,7 +1392,7 @@ int blbrs_reconstruct_dev_ptrs(blbrs_encoder* enc, uint8_t* const* shard_ptrs, s
     if ((rc = dc.enter(shard_ptrs[hp->in_idx[0]]))) return rc;
     rt::PtrLease lease;
     Stripes st;
-    if ((rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, &st.ptrs, &st.aligned)))
+    if ((rc = upload_ptrs(shard_ptrs, batch * n, static_cast<hipStream_t>(stream), lease, dc.dev, &st)))
         return rc;
     st.nshards = n;
     return dev_run(enc, dc.dev, key, *hp, st, batch, shard_len, Mode::kStore, nullptr, stream);
@@ -1441,7 +1452,7 @@ int blbrs_verify_dev_ptrs(blbrs_encoder* enc, const uint8_t* const* shard_ptrs, 
     rt::PtrLease lease;
     Stripes st;
     if ((rc = upload_ptrs(const_cast<uint8_t* const*>(shard_ptrs), batch * n, static_cast<hipStream_t>(stream),
-                          lease, &st.ptrs, &st.aligned)))
+                          lease, dc.dev, &st)))
         return rc;
     st.nshards = n;
     auto hp = enc->encode_plan();
@@ -1959,6 +1970,31 @@ int blbrs_get_device_stats(int device, blbrs_device_stats* out) {
 int blbrs_trim(void) {
     rt::trim_workers();
     rt::pool_trim();
+    return BLBRS_OK;
+}
+
+int blbrs_table_fault_take(int device, blbrs_table_fault* out, int* found) {
+    if (!out || !found || device < 0) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
+    *found = 0;
+    *out = blbrs_table_fault{};
+    uint32_t* rec = rt::device_fault_record(device);
+    if (!rec) return fail(BLBRS_ERR_HIP, "no fault record for device " + std::to_string(device));
+    volatile uint32_t* v = rec;
+    if (!v[0]) return BLBRS_OK;
+    const uint64_t e = (static_cast<uint64_t>(v[5]) << 32) | v[4];
+    out->stripe = v[1];
+    out->slot = v[2];
+    out->launch_tag = v[3];
+    out->entry_tag = static_cast<uint32_t>(e >> kPtrTagShift);
+    out->address = e & kPtrMask;
+    *found = 1;
+    for (int i = 0; i < rt::kFaultWords; ++i) v[i] = 0;
+    return BLBRS_OK;
+}
+
+int blbrs_debug_corrupt_next_table(int slot) {
+    if (slot < 0) return fail(BLBRS_ERR_INVALID_ARG, "negative slot");
+    rt::corrupt_next_table(slot);
     return BLBRS_OK;
 }
 

@@ -64,8 +64,6 @@ struct KArgs {
     uint64_t total_segs;
     const CrcConsts* c;
     uint32_t* raw;            // [(j * B + b) * nblocks + blk] * segs_per_block + s
-    uint32_t flags;           // tuning switches (BLBRS_EC_FLAGS): 1 = no CRC, 2 = plain stores, 4 = nt loads,
-                              // 8 = one segment per wave (non-persistent grid)
 };
 
 template <int LC>
@@ -86,8 +84,7 @@ __device__ __forceinline__ void load_row(const KArgs& a, const uint8_t* stripe, 
         const uint8_t* p = stripe + static_cast<uint64_t>(in_idx[c]) * a.shard_stride + row_off + lane_piece<LC>(lane);
 #pragma unroll
         for (int q = 0; q < LC / 16; ++q) {
-            const u32x4 v = (a.flags & 4u) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 1024 * q))
-                                           : *reinterpret_cast<const u32x4*>(p + 1024 * q);
+            const u32x4 v = *reinterpret_cast<const u32x4*>(p + 1024 * q);
             x[c][4 * q] = v.x;
             x[c][4 * q + 1] = v.y;
             x[c][4 * q + 2] = v.z;
@@ -183,10 +180,7 @@ __device__ __forceinline__ void encode_crc_segment(const KArgs& a, uint64_t g, u
 #pragma unroll
                 for (int u = 0; u < G::kQ; ++u) {
                     const u32x4 v = {acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]};
-                    if (a.flags & 2u)
-                        *reinterpret_cast<u32x4*>(q + 1024 * u) = v;
-                    else
-                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(q + 1024 * u));
+                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(q + 1024 * u));
                 }
             }
         } else {
@@ -200,7 +194,6 @@ __device__ __forceinline__ void encode_crc_segment(const KArgs& a, uint64_t g, u
                 for (int i = 0; i < G::kDw; ++i) __builtin_amdgcn_raw_buffer_store_b32(acc[j][i], rs, voff(o, i), 0, 0);
             }
         }
-        if (a.flags & 1u) return;
         // CRC: each lane takes its LC contiguous parity bytes (register transpose), then one
         // slicing-by-4 chain per parity row, chains interleaved for LDS latency.
 #pragma unroll
@@ -251,44 +244,6 @@ __device__ __forceinline__ void encode_crc_segment(const KArgs& a, uint64_t g, u
         for (int j = 0; j < MR; ++j) raw[j * raw_row] = crc[j];
 }
 
-// Tuning only (flag 16, no CRC, whole rows): the XCD's waves stream consecutive 4 KiB rows
-// (wave v takes rows lo + v, lo + v + xwaves, ...), the coding kernel's access pattern.
-template <int K, int MR, int LC>
-__device__ void rows_streaming(const KArgs& a, uint32_t lane, uint32_t v, uint32_t xcd, uint32_t nxcd, uint64_t xwaves) {
-    using G = Geo<LC>;
-    const uint64_t rps = a.S / G::kRow, total = rps * a.B;
-    const uint64_t lo = total * xcd / nxcd, hi = total * (xcd + 1) / nxcd;
-    const ci32 in_idx = as_const(a.in_idx);
-    const ci32 out_idx = as_const(a.out_idx);
-    for (uint64_t row = lo + v; row < hi; row += xwaves) {
-        const uint64_t b = row / rps;
-        const int64_t off = static_cast<int64_t>((row % rps) * G::kRow);
-        uint8_t* stripe = a.base + b * a.stripe_stride;
-        uint32_t x[K][G::kDw];
-        load_row<K, LC>(a, stripe, in_idx, off, lane, x);
-        cu32 tables = as_const(a.tables);
-        asm volatile("" : "+s"(tables));
-        uint32_t acc[MR][G::kDw] = {};
-#pragma unroll
-        for (int c = 0; c + 1 < K; c += 2) {
-            cu32 tp = tables;
-            asm volatile("" : "+s"(tp));
-            madd2_dw<MR, G::kDw>(x[c], [&](int rr) { return tp + (rr * K + c) * 5; }, x[c + 1],
-                                 [&](int rr) { return tp + (rr * K + c + 1) * 5; }, acc);
-        }
-        if constexpr (K & 1)
-            madd_dw<MR, G::kDw>(x[K - 1], [&](int rr) { return tables + (rr * K + K - 1) * 5; }, acc);
-#pragma unroll
-        for (int j = 0; j < MR; ++j) {
-            uint8_t* q = stripe + static_cast<uint64_t>(out_idx[j]) * a.shard_stride + off + lane_piece<LC>(lane);
-#pragma unroll
-            for (int u = 0; u < G::kQ; ++u)
-                __builtin_nontemporal_store(u32x4{acc[j][4 * u], acc[j][4 * u + 1], acc[j][4 * u + 2], acc[j][4 * u + 3]},
-                                            reinterpret_cast<u32x4*>(q + 1024 * u));
-        }
-    }
-}
-
 // Persistent: one workgroup per CU (the banked tables are built once), and its 8 waves walk
 // segments independently with no further barrier.  The waves of XCD x (workgroups are
 // dealt round-robin over the 8 XCDs) cover the x-th eighth of the segments, interleaved
@@ -307,10 +262,6 @@ __global__ __launch_bounds__(kEcThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     const uint32_t xcd = blockIdx.x % nxcd;
     const uint64_t xwaves = static_cast<uint64_t>(gridDim.x / nxcd) * kWaves;
     const uint64_t lo = a.total_segs * xcd / nxcd, hi = a.total_segs * (xcd + 1) / nxcd;
-    if (a.flags & 16u) {
-        rows_streaming<K, MR, LC>(a, lane, (blockIdx.x / nxcd) * kWaves + wave, xcd, nxcd, xwaves);
-        return;
-    }
     for (uint64_t g = lo + (blockIdx.x / nxcd) * kWaves + wave; g < hi; g += xwaves)
         encode_crc_segment<K, MR, LC>(a, g, lane, lt);
 }
@@ -398,19 +349,17 @@ hipError_t launch_encode_crc(const EncodeCrcArgs& in, hipStream_t stream) {
     a.segs_per_block = static_cast<uint32_t>((a.block + kSeg - 1) / kSeg);
     a.total_segs = static_cast<uint64_t>(in.B) * a.nblocks * a.segs_per_block;
     a.c = c;
-    if (const long f = tune::get(tune::kEcFlags)) a.flags = static_cast<uint32_t>(f);
     const uint64_t total_blocks = static_cast<uint64_t>(in.rows) * in.B * a.nblocks;
     if (a.total_segs * kWaves > 0x7FFFFFFFull || total_blocks * a.segs_per_block > 0x7FFFFFFFull)
         return hipErrorInvalidValue;
     if ((e = hipMallocAsync(reinterpret_cast<void**>(&a.raw), total_blocks * a.segs_per_block * 4, stream)) !=
         hipSuccess)
         return e;
-    // Persistent grid: one workgroup per CU (flag 8 = one segment per wave instead, for A/B).
+    // Persistent grid: one workgroup per CU.
     static thread_local int cus = 0;
     if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0))
         cus = 256;
-    uint64_t grid = (a.total_segs + kWaves - 1) / kWaves;
-    if (!(a.flags & 8u)) grid = std::min<uint64_t>(grid, static_cast<uint64_t>(cus));
+    uint64_t grid = std::min<uint64_t>((a.total_segs + kWaves - 1) / kWaves, static_cast<uint64_t>(cus));
     if (grid >= 8) grid = (grid + 7) & ~uint64_t{7};  // whole XCD rounds (the kernel splits by blockIdx % 8)
     hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEcThreads), kEcLds, stream, a);
     e = hipGetLastError();

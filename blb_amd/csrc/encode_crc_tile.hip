@@ -818,9 +818,7 @@ hipError_t launch_encode_crc_tile(const EncodeCrcArgs& in, hipStream_t stream) {
             hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), 0, stream, a);
     }
 #else
-    unsigned occ = 0;  // A/B knob, as rs_kernels.hip: dynamic LDS per workgroup of the network launches
-    if (const long v = cm ? tune::get(tune::kOccLdsEct) : 0; v > 0) occ = static_cast<unsigned>(std::min(v, 65536L));
-    if (groups) hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), occ, stream, a);
+    if (groups) hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(groups)), dim3(kTThreads), 0, stream, a);
 #endif
     e = hipGetLastError();
     if (e == hipSuccess && a.tps != a.tps_full) {

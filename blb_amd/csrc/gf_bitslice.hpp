@@ -188,7 +188,12 @@ inline bool is_parity_rows(const uint8_t* rows, int nrows, int k) {
 // threshold).  Where the table kernel already runs at the access pattern's speed (RS(6,3)) it
 // folds each input pair as its loads land and stays 2-5 % ahead of the network.
 // Knob BLBRS_BITSLICE (tuning.hpp; A/B runs): 0 = never, 2 = every compiled shape.
-inline int mode() { return static_cast<int>(tune::get(tune::kBitslice)); }
+// 0 and 2 as set; any other value is the default 1 (a stray value must not switch the compiled
+// encode networks off, which only the m == 1 / m == 2 branches of use() would notice).
+inline int mode() {
+    const long v = tune::get(tune::kBitslice);
+    return v == 0 || v == 2 ? static_cast<int>(v) : 1;
+}
 inline bool use(bool parity, int k, int rows, int wide) {
     if (!parity) return false;
     const int m = mode();

@@ -11,8 +11,6 @@
 // leaves the source buffer's pages.  Region heads/tails (< 16 bytes) go byte by byte.
 #include "pack.hpp"
 
-#include "tuning.hpp"
-
 namespace blbrs {
 namespace {
 
@@ -58,18 +56,14 @@ __device__ __forceinline__ V4 funnel(const V4& a, const V4& b, uint32_t q, uint3
     return o;
 }
 
-template <bool NT>
-__device__ __forceinline__ V4 ld(const V4* p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-
 // Copy n bytes src -> dst with the whole workgroup (n, src, dst uniform).  Chunk i (16
-// destination bytes) is lane i % 256's, UNR chunks per lane in flight.  A misaligned source is
-// read as aligned blocks: lane i loads block i and takes block i + 1 from the next lane (DPP)
-// -- one load per chunk -- except lane 63 of each wave, whose next block is another wave's and
-// is loaded (DPP = false: every lane loads both blocks, the round-2 kernel).
-template <bool DPP, bool NT, int UNR>
+// destination bytes) is lane i % 256's, kUnr chunks per lane in flight (the whole 64 KiB tile).
+// Loads stay cached: nontemporal loads were 3-28 % slower box to box (profiles/r03/pack/).  A
+// misaligned source is read as aligned blocks: lane i loads block i and takes block i + 1 from
+// the next lane (DPP) -- one load per chunk -- except lane 63 of each wave, whose next block is
+// another wave's and is loaded.  (Round 2 loaded both blocks in every lane: 15.8 vs 13.6 ms.)
+constexpr int kUnr = 16;
+
 __device__ void copy_region(uint8_t* dst, const uint8_t* src, uint64_t n) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -83,42 +77,34 @@ __device__ void copy_region(uint8_t* dst, const uint8_t* src, uint64_t n) {
     const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s) & 15u);
     const V4* sa = reinterpret_cast<const V4*>(s - mis);  // aligned block holding s[0]
     if (mis == 0) {
-        for (uint64_t c = tid; c < nb; c += UNR * kPackThreads) {
-            V4 v[UNR];
+        for (uint64_t c = tid; c < nb; c += kUnr * kPackThreads) {
+            V4 v[kUnr];
 #pragma unroll
-            for (int u = 0; u < UNR; ++u)
-                if (c + u * kPackThreads < nb) v[u] = ld<NT>(sa + c + u * kPackThreads);
+            for (int u = 0; u < kUnr; ++u)
+                if (c + u * kPackThreads < nb) v[u] = sa[c + u * kPackThreads];
 #pragma unroll
-            for (int u = 0; u < UNR; ++u)
+            for (int u = 0; u < kUnr; ++u)
                 if (c + u * kPackThreads < nb) __builtin_nontemporal_store(v[u], d + c + u * kPackThreads);
         }
     } else {
         const uint32_t q = mis >> 2, r = mis & 3u;
         // Every block up to nb holds wanted bytes (mis > 0: the last wanted byte lies in block
         // nb), so no read leaves them.
-        for (uint64_t c = tid; c < nb + (DPP && nb > 0 ? 1 : 0); c += UNR * kPackThreads) {
-            V4 v[UNR], h[UNR];
+        for (uint64_t c = tid; c < nb + (nb > 0 ? 1 : 0); c += kUnr * kPackThreads) {
+            V4 v[kUnr], h[kUnr];
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) v[u] = h[u] = V4{0u, 0u, 0u, 0u};
+            for (int u = 0; u < kUnr; ++u) v[u] = h[u] = V4{0u, 0u, 0u, 0u};
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) {
+            for (int u = 0; u < kUnr; ++u) {
                 const uint64_t i = c + u * kPackThreads;
-                if constexpr (DPP) {
-                    if (i <= nb) v[u] = ld<NT>(sa + i);
-                    if (lane == 63u && i < nb) h[u] = ld<NT>(sa + i + 1);
-                } else if (i < nb) {
-                    v[u] = ld<NT>(sa + i);
-                    h[u] = ld<NT>(sa + i + 1);
-                }
+                if (i <= nb) v[u] = sa[i];
+                if (lane == 63u && i < nb) h[u] = sa[i + 1];
             }
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) {
+            for (int u = 0; u < kUnr; ++u) {
                 const uint64_t i = c + u * kPackThreads;
-                V4 hb = h[u];
-                if constexpr (DPP) {
-                    const V4 nx = rol1(v[u]);
-                    if (lane != 63u) hb = nx;
-                }
+                const V4 nx = rol1(v[u]);
+                const V4 hb = lane != 63u ? nx : h[u];
                 if (i < nb) __builtin_nontemporal_store(funnel(v[u], hb, q, r), d + i);
             }
         }
@@ -140,15 +126,12 @@ __device__ void zero_region(uint8_t* dst, uint64_t n) {
     if (tid < tail) dst[head + (nb << 4) + tid] = 0;
 }
 
-// REMAP: each XCD takes a contiguous eighth of the tiles (blocks are dealt round-robin over
-// the 8 XCDs), so the workgroups resident on one XCD stream neighbouring tiles.
-template <bool DPP, bool NT, int UNR, bool REMAP>
+// Each XCD takes a contiguous eighth of the tiles (blocks are dealt round-robin over the 8
+// XCDs), so the workgroups resident on one XCD stream neighbouring tiles.
 __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
     uint32_t t = blockIdx.x;
-    if constexpr (REMAP) {
-        t = (t % 8u) * (gridDim.x / 8u) + t / 8u;
-        if (t >= a.npieces * a.tiles_per_piece) return;
-    }
+    t = (t % 8u) * (gridDim.x / 8u) + t / 8u;
+    if (t >= a.npieces * a.tiles_per_piece) return;
     const uint32_t piece = t / a.tiles_per_piece;
     const uint64_t t0 = static_cast<uint64_t>(t % a.tiles_per_piece) * kPackTile;
     const uint64_t t1 = t0 + kPackTile < a.piece_len ? t0 + kPackTile : a.piece_len;
@@ -173,7 +156,7 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
         if (off <= cur) {  // inside extent e
             const uint64_t end = off + ex[4 * e + 2] < t1 ? off + ex[4 * e + 2] : t1;
             const uint8_t* src = reinterpret_cast<const uint8_t*>(ex[4 * e]);
-            copy_region<DPP, NT, UNR>(d + cur, src + (cur - off), end - cur);
+            copy_region(d + cur, src + (cur - off), end - cur);
             cur = end > cur ? end : cur;
             ++e;
         } else {  // hole or pad up to the next extent / tile end
@@ -181,29 +164,6 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackArgs a) {
             zero_region(d + cur, end - cur);
             cur = end;
         }
-    }
-}
-
-using PackFn = void (*)(PackArgs);
-
-// Variants (A/B knob BLBRS_PACK_VARIANT, tuning.hpp; tools/pack_ab.py,
-// profiles/r03/pack/): 6 = the default: XCD map, the whole 64 KiB tile (16 chunks per lane)
-// in flight, cached loads, DPP neighbour block; 0 = the round-2 kernel (two loads per
-// misaligned chunk, 4 chunks per lane, no XCD map); 8 = 6 with nontemporal loads and 8 chunks;
-// 10 = 6 without the DPP exchange.  bench.py's layout, RS(6,3) B=1024 (88 GB): 0 -> 6 = 15.8
-// -> 13.6 ms (6.5 TB/s), distinct sources 16.3 -> 13.9 ms.
-#ifndef BLBRS_PACK_DEFAULT
-#define BLBRS_PACK_DEFAULT 6
-#endif
-PackFn pick_pack(bool& remap) {
-    const long knob = tune::get(tune::kPackVariant);  // BLBRS_PACK_VARIANT (tuning.hpp)
-    const int v = knob >= 0 ? static_cast<int>(knob) : BLBRS_PACK_DEFAULT;
-    remap = v != 0;
-    switch (v) {
-        case 0: return pack_kernel<false, false, 4, false>;
-        case 8: return pack_kernel<true, true, 8, true>;
-        case 10: return pack_kernel<false, false, 16, true>;
-        default: return pack_kernel<true, false, 16, true>;
     }
 }
 
@@ -220,11 +180,8 @@ hipError_t pack_pieces(uint8_t* dst, uint64_t dst_stride, uint64_t npieces, uint
     }
     PackArgs a{dst, dst_stride, piece_len, static_cast<uint32_t>(npieces), static_cast<uint32_t>(tpp), table_dev,
                per_group, group_stride};
-    bool remap = false;
-    const PackFn fn = pick_pack(remap);
-    uint64_t grid = tpp * npieces;
-    if (remap) grid = (grid + 7) & ~uint64_t{7};  // a multiple of 8 blocks; the extra ones exit
-    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kPackThreads), 0, stream, a);
+    const uint64_t grid = (tpp * npieces + 7) & ~uint64_t{7};  // a multiple of 8 blocks; the extra ones exit
+    hipLaunchKernelGGL(pack_kernel, dim3(static_cast<unsigned>(grid)), dim3(kPackThreads), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -328,10 +328,8 @@ using KernelFn = void (*)(PEArgs);
 constexpr int pe_u(uint32_t k) { return k <= 6 ? BLBRS_PE_U_NARROW : BLBRS_PE_U_WIDE; }
 
 // The network runs at U = 2 for every k: it holds fewer registers than the table multiply
-// (RS(12,5) 141 at U = 1 with tables).  BLBRS_PE_CM_WIDE=0 (A/B) keeps wide k on the U = 1
-// table kernel.
-bool cm_wide() { return tune::get(tune::kPeCmWide) != 0; }
-int tile_u(uint32_t k, bool cm) { return cm && (k <= 6 || cm_wide()) ? 2 : pe_u(k); }
+// (RS(12,5) 141 at U = 1 with tables).
+int tile_u(uint32_t k, bool cm) { return cm ? 2 : pe_u(k); }
 
 template <int K, int MR>
 KernelFn pick_cm(bool cm) {

@@ -59,7 +59,40 @@ __device__ __forceinline__ uint8_t* shard_ptr(const CodeArgs& a, uint32_t b, int
         return a.base + static_cast<uint64_t>(b) * a.stripe_stride +
                static_cast<uint64_t>(idx) * a.shard_stride;
     else
-        return reinterpret_cast<uint8_t*>(as_const(a.ptrs)[static_cast<uint64_t>(b) * a.nshards + idx]);
+        return reinterpret_cast<uint8_t*>(as_const(a.ptrs)[static_cast<uint64_t>(b) * a.nshards + idx] & kPtrMask);
+}
+
+// Pointer-table addressing: every entry this pass reads or writes for stripe b must carry the
+// table's tag (the host writes it into bits 48-63 of each entry, runtime.hpp TableFault).  An
+// entry from another upload, or not from an upload at all, is never dereferenced: the stripe's
+// tile is skipped and the entry recorded for the host, which fails the call naming the slot.
+// Scalar loads of the entries the tile reads anyway; nothing for strided addressing.
+template <int ADDR>
+__device__ __forceinline__ bool stripe_table_ok(const CodeArgs& a, uint32_t b) {
+    if constexpr (ADDR == 0) {
+        return true;
+    } else {
+        const cu64 row = as_const(a.ptrs) + static_cast<uint64_t>(b) * a.nshards;
+        const ci32 in_idx = as_const(a.in_idx), out_idx = as_const(a.out_idx);
+        const int n = a.k + a.rows;
+        for (int j = 0; j < n; ++j) {
+            const int idx = j < a.k ? in_idx[j] : out_idx[j - a.k];
+            const uint64_t e = row[idx];
+            if (static_cast<uint32_t>(e >> kPtrTagShift) != a.ptr_tag) {
+                if (threadIdx.x == 0) {  // vector stores to the host-mapped record, header last
+                    a.fault[1] = b;
+                    a.fault[2] = static_cast<uint32_t>(idx);
+                    a.fault[3] = a.ptr_tag;
+                    a.fault[4] = static_cast<uint32_t>(e);
+                    a.fault[5] = static_cast<uint32_t>(e >> 32);
+                    __threadfence_system();
+                    a.fault[0] = 1u;
+                }
+                return false;
+            }
+        }
+        return true;
+    }
 }
 
 // 16-byte global load/store; NT bit 0 = nontemporal loads, bit 1 = nontemporal stores
@@ -175,6 +208,7 @@ void rs_code_kernel(CodeArgs a) {
     for (uint32_t t = first; t < total; t += gridDim.x) {
         const uint32_t b = t / a.tiles_per_stripe;
         const uint64_t tile_off = static_cast<uint64_t>(t - b * a.tiles_per_stripe) * kTile;
+        if (!stripe_table_ok<ADDR>(a, b)) continue;
         if (!aligned || tile_off + kTile > a.S) {
             code_tile_slow<MR, MODE, ADDR, U>(a, b, tile_off);
             continue;

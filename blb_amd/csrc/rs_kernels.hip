@@ -97,14 +97,6 @@ Choice pick(int k, int rows, Mode mode, bool strided, bool cm = false) {
     return strided ? pick_k<2, 0>(k, rows, false) : pick_k<2, 1>(k, rows, false);
 }
 
-// A/B knob BLBRS_OCC_LDS=<bytes> (tuning.hpp, <= 64 KiB) reserves that much dynamic LDS per
-// workgroup of the network launches, capping workgroups per CU (160 KiB / bytes).
-unsigned occupancy_lds(bool cm) {
-    if (!cm) return 0;
-    const long v = tune::get(tune::kOccLds);
-    return v > 0 && v <= 65536 ? static_cast<unsigned>(v) : 0u;
-}
-
 }  // namespace
 
 hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc::NetKernel* net) {
@@ -114,7 +106,7 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc:
     if (args.B == 0 || args.S == 0) return hipSuccess;
     Choice ch = pick(args.k, args.rows, mode, args.base != nullptr, bs::use(args.parity, args.k, args.rows, bs::kWideCode));
     // A run-time network replaces the table kernel once loaded (the caller asks for one only where
-    // no compiled encode network applies, or for the BLBRS_RTC_ENCODE A/B).
+    // no compiled encode network applies).
     hipFunction_t rfn = rtc::ready(net);
     if (rfn) {
         ch.u = net->u;
@@ -142,10 +134,9 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc:
         hipError_t e;
         if (rfn) {
             void* params[] = {&a};
-            e = hipModuleLaunchKernel(rfn, static_cast<unsigned>(grid), 1, 1, kThreads, 1, 1, occupancy_lds(true), stream,
-                                      params, nullptr);
+            e = hipModuleLaunchKernel(rfn, static_cast<unsigned>(grid), 1, 1, kThreads, 1, 1, 0, stream, params, nullptr);
         } else {
-            hipLaunchKernelGGL(ch.fn, dim3(static_cast<unsigned>(grid)), dim3(kThreads), occupancy_lds(ch.cm), stream, a);
+            hipLaunchKernelGGL(ch.fn, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, stream, a);
             e = hipGetLastError();
         }
         if (e != hipSuccess) return e;

@@ -30,7 +30,17 @@ struct CodeArgs {
     int32_t nstore;           // kStoreVerify: rows [0, nstore) are stored, the rest compared
     int32_t parity;           // rows = encode parity rows 0..rows-1 of k: the compiled network
                               //   (gf_bitslice.hpp) where the shape has one
+    // Pointer-table check (ADDR = 1): every entry carries its table's 16-bit tag in bits 48-63
+    // (TableFault in runtime.hpp).  A stripe whose entries do not all carry ptr_tag is not
+    // touched; the kernel records the first entry it finds wrong in *fault (host-mapped).
+    uint32_t* fault;          // [8]: valid, stripe, slot, expected tag, entry lo, entry hi
+    uint32_t ptr_tag;
 };
+
+// Table entries: the device address in bits 0-47 (every GPU and host address the runtime hands
+// out is below 2^48), the table's tag above.
+constexpr int kPtrTagShift = 48;
+constexpr uint64_t kPtrMask = (uint64_t{1} << kPtrTagShift) - 1;
 
 constexpr int kThreads = 256;
 constexpr int kBytesPerThread = 16;                       // one dwordx4 per shard per lane

@@ -15,6 +15,7 @@
 #include <thread>
 #include <vector>
 
+#include <dlfcn.h>
 #include <unistd.h>
 
 #include "gf256.hpp"
@@ -42,109 +43,62 @@ constexpr size_t kMaxEntries = 512;  // kernels kept per process; past it, passe
 // --- network generation --------------------------------------------------------------------
 
 // Output plane (r, p) = XOR of input planes (c, q) with bit p of coef[r][c] * 2^q set
-// (multiplying by a constant is GF(2)-linear), emitted as a chain of v_bitop3 XOR3s.  With `cse`
-// (knob BLBRS_RTC_CSE, off by default), a pair of signals that appears in three or more outputs
-// becomes one temporary first (greedy, most frequent pair first, temporaries may pair again:
-// Paar's heuristic); an output of T signals then costs floor(T / 2) XOR3s and a temporary one
-// XOR, and the cheaper form is emitted.  Measured: it does not pay -- LLVM's reassociation
-// already shares terms (the same static VALU count either way), and the long-lived temporaries
-// take RS(12,5)'s recovery kernel from 156 VGPRs to 252-280 (occupancy 3 -> 2 or 1; 7-35 %
-// slower launches, profiles/r04/rtc_ab).
-struct Net {
-    int nin = 0;
-    std::vector<std::pair<int, int>> temps;  // signal nin + i = first ^ second
-    std::vector<std::vector<int>> outs;      // per output plane, its signals
+// (multiplying by a constant is GF(2)-linear), emitted as a chain of v_bitop3 XOR3s.  No explicit
+// shared temporaries: LLVM's reassociation already shares terms between output planes (the static
+// VALU count is the same with Paar-style pair sharing), and long-lived temporaries took RS(12,5)'s
+// recovery kernel from 156 VGPRs to 252-280 and 7-35 % slower launches (round 4,
+// profiles/r04/rtc_ab; the variant is no longer built).
+using Planes = std::vector<std::vector<int>>;  // per output plane, its input signals c * 8 + q
 
-    int ops() const {
-        int n = static_cast<int>(temps.size());
-        for (const auto& o : outs) n += o.size() <= 1 ? 0 : static_cast<int>(o.size()) / 2;
-        return n;
-    }
-};
-
-Net plain_net(int k, int rows, const uint8_t* coef) {
+Planes plane_terms(int k, int rows, const uint8_t* coef) {
     const GF& g = gf();
-    Net net;
-    net.nin = 8 * k;
-    net.outs.resize(static_cast<size_t>(rows) * 8);
+    Planes outs(static_cast<size_t>(rows) * 8);
     for (int r = 0; r < rows; ++r)
         for (int c = 0; c < k; ++c)
             for (int q = 0; q < 8; ++q) {
                 const uint8_t col = g.mul(coef[r * k + c], static_cast<uint8_t>(1u << q));
                 for (int p = 0; p < 8; ++p)
-                    if ((col >> p) & 1u) net.outs[r * 8 + p].push_back(c * 8 + q);
+                    if ((col >> p) & 1u) outs[r * 8 + p].push_back(c * 8 + q);
             }
-    return net;
+    return outs;
 }
 
-void share_pairs(Net& net) {
-    for (;;) {
-        const int nsig = net.nin + static_cast<int>(net.temps.size());
-        std::vector<int> cnt(static_cast<size_t>(nsig) * nsig, 0);
-        for (auto& o : net.outs) {
-            std::sort(o.begin(), o.end());
-            for (size_t i = 0; i < o.size(); ++i)
-                for (size_t j = i + 1; j < o.size(); ++j) ++cnt[static_cast<size_t>(o[i]) * nsig + o[j]];
-        }
-        int best = 0, ba = -1, bb = -1;
-        for (int a = 0; a < nsig; ++a)
-            for (int b = a + 1; b < nsig; ++b)
-                if (cnt[static_cast<size_t>(a) * nsig + b] > best) {
-                    best = cnt[static_cast<size_t>(a) * nsig + b];
-                    ba = a;
-                    bb = b;
-                }
-        if (best < 3) return;
-        const int s = nsig;
-        net.temps.emplace_back(ba, bb);
-        for (auto& o : net.outs) {
-            auto ia = std::find(o.begin(), o.end(), ba), ib = std::find(o.begin(), o.end(), bb);
-            if (ia == o.end() || ib == o.end()) continue;
-            o.erase(std::remove_if(o.begin(), o.end(), [&](int v) { return v == ba || v == bb; }), o.end());
-            o.push_back(s);
-        }
-    }
+int xor_ops(const Planes& outs) {
+    int n = 0;
+    for (const auto& o : outs) n += o.size() <= 1 ? 0 : static_cast<int>(o.size()) / 2;
+    return n;
 }
 
-std::string sig_name(const Net& net, int s) {
-    if (s < net.nin) return "x[" + std::to_string(s / 8) + "][" + std::to_string(s % 8) + "]";
-    return "t" + std::to_string(s - net.nin);
-}
+std::string sig_name(int s) { return "x[" + std::to_string(s / 8) + "][" + std::to_string(s % 8) + "]"; }
 
 // One output plane: its signals folded by XOR3s.
-std::string fold_expr(const Net& net, const std::vector<int>& s) {
+std::string fold_expr(const std::vector<int>& s) {
     if (s.empty()) return "0u";
-    if (s.size() == 1) return sig_name(net, s[0]);
-    if (s.size() == 2) return sig_name(net, s[0]) + " ^ " + sig_name(net, s[1]);
-    std::string e = "xor3(" + sig_name(net, s[0]) + ", " + sig_name(net, s[1]) + ", " + sig_name(net, s[2]) + ")";
+    if (s.size() == 1) return sig_name(s[0]);
+    if (s.size() == 2) return sig_name(s[0]) + " ^ " + sig_name(s[1]);
+    std::string e = "xor3(" + sig_name(s[0]) + ", " + sig_name(s[1]) + ", " + sig_name(s[2]) + ")";
     size_t i = 3;
-    for (; i + 1 < s.size(); i += 2) e = "xor3(" + e + ", " + sig_name(net, s[i]) + ", " + sig_name(net, s[i + 1]) + ")";
-    if (i < s.size()) e = "(" + e + " ^ " + sig_name(net, s[i]) + ")";
+    for (; i + 1 < s.size(); i += 2) e = "xor3(" + e + ", " + sig_name(s[i]) + ", " + sig_name(s[i + 1]) + ")";
+    if (i < s.size()) e = "(" + e + " ^ " + sig_name(s[i]) + ")";
     return e;
 }
 
-std::string emit(const Net& net, int k, int rows) {
+std::string emit(const Planes& outs, int k, int rows) {
     std::string o;
     o += "struct BlbrsNet {\n  template <int MR>\n  __device__ static __forceinline__ void rows(const uint32_t (&x)[" +
          std::to_string(k) + "][8], uint32_t (&o)[MR][8]) {\n";
     o += "    static_assert(MR == " + std::to_string(rows) + ", \"rows\");\n";
     o += "    using blbrs::dev::xor3;\n";
-    for (size_t i = 0; i < net.temps.size(); ++i)
-        o += "    const uint32_t t" + std::to_string(i) + " = " + sig_name(net, net.temps[i].first) + " ^ " +
-             sig_name(net, net.temps[i].second) + ";\n";
     for (int r = 0; r < rows; ++r)
         for (int p = 0; p < 8; ++p)
-            o += "    o[" + std::to_string(r) + "][" + std::to_string(p) + "] = " + fold_expr(net, net.outs[r * 8 + p]) + ";\n";
+            o += "    o[" + std::to_string(r) + "][" + std::to_string(p) + "] = " + fold_expr(outs[r * 8 + p]) + ";\n";
     o += "#pragma unroll\n    for (int r = 0; r < MR; ++r) blbrs::bs::transpose8(o[r]);\n  }\n";
     // each<MR>(x, f): the same rows one at a time, f(r, row) as soon as row r is in byte form.
     o += "  template <int MR, class F>\n  __device__ static __forceinline__ void each(const uint32_t (&x)[" + std::to_string(k) +
          "][8], F& f) {\n    static_assert(MR == " + std::to_string(rows) + ", \"rows\");\n    using blbrs::dev::xor3;\n";
-    for (size_t i = 0; i < net.temps.size(); ++i)
-        o += "    const uint32_t t" + std::to_string(i) + " = " + sig_name(net, net.temps[i].first) + " ^ " +
-             sig_name(net, net.temps[i].second) + ";\n";
     for (int r = 0; r < rows; ++r) {
         o += "    {\n      uint32_t o[8];\n";
-        for (int p = 0; p < 8; ++p) o += "      o[" + std::to_string(p) + "] = " + fold_expr(net, net.outs[r * 8 + p]) + ";\n";
+        for (int p = 0; p < 8; ++p) o += "      o[" + std::to_string(p) + "] = " + fold_expr(outs[r * 8 + p]) + ";\n";
         o += "      blbrs::bs::transpose8(o);\n      f(" + std::to_string(r) + ", o);\n    }\n";
     }
     o += "  }\n};\n";
@@ -204,8 +158,64 @@ std::mutex& comgr_mu() {
     return *m;
 }
 
+// hipRTC, opened on first use (dlopen), not linked: a process that never asks for a run-time
+// network -- the default, BLBRS_RTC = 0 -- never maps hipRTC or the LLVM (comgr) it loads.
+struct Hiprtc {
+    decltype(&hiprtcCreateProgram) create = nullptr;
+    decltype(&hiprtcAddNameExpression) add_name = nullptr;
+    decltype(&hiprtcCompileProgram) compile = nullptr;
+    decltype(&hiprtcGetProgramLogSize) log_size = nullptr;
+    decltype(&hiprtcGetProgramLog) log = nullptr;
+    decltype(&hiprtcGetErrorString) error_string = nullptr;
+    decltype(&hiprtcGetCodeSize) code_size = nullptr;
+    decltype(&hiprtcGetCode) code = nullptr;
+    decltype(&hiprtcGetLoweredName) lowered_name = nullptr;
+    decltype(&hiprtcDestroyProgram) destroy = nullptr;
+    std::string error;  // why it is unavailable ("" when loaded)
+};
+
+template <class F>
+bool sym(void* h, const char* name, F* out, std::string* err) {
+    *out = reinterpret_cast<F>(dlsym(h, name));
+    if (!*out && err->empty()) *err = std::string("hipRTC: no symbol ") + name;
+    return *out != nullptr;
+}
+
+const Hiprtc& hiprtc() {
+    static const Hiprtc* api = [] {
+        auto* a = new Hiprtc;  // process lifetime, as the library handle
+        void* h = dlopen("libhiprtc.so.7", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("libhiprtc.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            a->error = std::string("hipRTC not loadable: ") + (e ? e : "dlopen failed");
+            return a;
+        }
+        std::string err;
+        int ok = 1;  // every symbol is looked up, so the error names the first missing one
+        ok &= sym(h, "hiprtcCreateProgram", &a->create, &err);
+        ok &= sym(h, "hiprtcAddNameExpression", &a->add_name, &err);
+        ok &= sym(h, "hiprtcCompileProgram", &a->compile, &err);
+        ok &= sym(h, "hiprtcGetProgramLogSize", &a->log_size, &err);
+        ok &= sym(h, "hiprtcGetProgramLog", &a->log, &err);
+        ok &= sym(h, "hiprtcGetErrorString", &a->error_string, &err);
+        ok &= sym(h, "hiprtcGetCodeSize", &a->code_size, &err);
+        ok &= sym(h, "hiprtcGetCode", &a->code, &err);
+        ok &= sym(h, "hiprtcGetLoweredName", &a->lowered_name, &err);
+        ok &= sym(h, "hiprtcDestroyProgram", &a->destroy, &err);
+        if (!ok) a->error = err;
+        return a;
+    }();
+    return *api;
+}
+
 // Compile (outside the state lock); nullptr + log on failure.
 std::shared_ptr<Compiled> compile(const std::string& src, const std::string& name_expr, std::string* log) {
+    const Hiprtc& rt = hiprtc();
+    if (!rt.error.empty()) {
+        *log = rt.error;
+        return nullptr;
+    }
     std::lock_guard<std::mutex> comgr(comgr_mu());
     std::vector<const char*> names, srcs;
     for (const Header& h : kHeaders) {
@@ -213,36 +223,36 @@ std::shared_ptr<Compiled> compile(const std::string& src, const std::string& nam
         srcs.push_back(h.src);
     }
     hiprtcProgram prog = nullptr;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "blbrs_net.hip", static_cast<int>(names.size()), srcs.data(),
-                            names.data()) != HIPRTC_SUCCESS) {
+    if (rt.create(&prog, src.c_str(), "blbrs_net.hip", static_cast<int>(names.size()), srcs.data(), names.data()) !=
+        HIPRTC_SUCCESS) {
         *log = "hiprtcCreateProgram failed";
         return nullptr;
     }
-    hiprtcAddNameExpression(prog, name_expr.c_str());
+    rt.add_name(prog, name_expr.c_str());
     const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    const hiprtcResult rc = rt.compile(prog, 3, opts);
     std::shared_ptr<Compiled> out;
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
-        hiprtcGetProgramLogSize(prog, &n);
+        rt.log_size(prog, &n);
         std::string l(n, '\0');
-        if (n) hiprtcGetProgramLog(prog, &l[0]);
-        *log = std::string(hiprtcGetErrorString(rc)) + ": " + l;
+        if (n) rt.log(prog, &l[0]);
+        *log = std::string(rt.error_string(rc)) + ": " + l;
     } else {
         out = std::make_shared<Compiled>();
         size_t n = 0;
-        hiprtcGetCodeSize(prog, &n);
+        rt.code_size(prog, &n);
         out->code.resize(n);
-        hiprtcGetCode(prog, out->code.data());
+        rt.code(prog, out->code.data());
         const char* lowered = nullptr;
-        if (hiprtcGetLoweredName(prog, name_expr.c_str(), &lowered) != HIPRTC_SUCCESS || !lowered) {
+        if (rt.lowered_name(prog, name_expr.c_str(), &lowered) != HIPRTC_SUCCESS || !lowered) {
             *log = "hiprtcGetLoweredName failed for " + name_expr;
             out.reset();
         } else {
             out->lowered = lowered;
         }
     }
-    hiprtcDestroyProgram(&prog);
+    rt.destroy(&prog);
     exit_hook_again();
     return out;
 }
@@ -351,10 +361,12 @@ void at_exit() {
 void exit_hook() {
     static std::once_flag once;
     std::call_once(once, [] {
-        std::lock_guard<std::mutex> comgr(comgr_mu());
-        hiprtcProgram p = nullptr;
-        if (hiprtcCreateProgram(&p, "", "blbrs_load.hip", 0, nullptr, nullptr) == HIPRTC_SUCCESS)
-            hiprtcDestroyProgram(&p);
+        const Hiprtc& rt = hiprtc();
+        if (rt.error.empty()) {
+            std::lock_guard<std::mutex> comgr(comgr_mu());
+            hiprtcProgram p = nullptr;
+            if (rt.create(&p, "", "blbrs_load.hip", 0, nullptr, nullptr) == HIPRTC_SUCCESS) rt.destroy(&p);
+        }
         std::atexit(at_exit);
     });
 }
@@ -366,15 +378,21 @@ void exit_hook_again() {
     if (n.fetch_add(1, std::memory_order_relaxed) < 4096) std::atexit(at_exit);
 }
 
-std::string kernel_source(int k, int rows, const uint8_t* coef, bool cse, int* ops) {
-    Net plain = plain_net(k, rows, coef);
-    Net net = plain;
-    if (cse) {
-        share_pairs(net);
-        if (net.ops() >= plain.ops()) net = plain;
-    }
-    if (ops) *ops = net.ops();
-    return emit(net, k, rows);
+std::string kernel_source(int k, int rows, const uint8_t* coef, int* ops) {
+    const Planes outs = plane_terms(k, rows, coef);
+    if (ops) *ops = xor_ops(outs);
+    return emit(outs, k, rows);
+}
+
+// Handed out once kMaxEntries kernels exist: a pass's slot caches it, so the pass stays on tables
+// without generating its source again on every launch.
+NetKernel* disabled() {
+    static NetKernel* nk = [] {
+        auto* p = new NetKernel;
+        p->state.store(-1);
+        return p;
+    }();
+    return nk;
 }
 
 }  // namespace
@@ -387,9 +405,7 @@ bool eligible(int k, int rows) {
            k + rows > tune::get(tune::kRtcWide);
 }
 
-std::string network_source(int k, int rows, const uint8_t* coef, bool cse, int* ops) {
-    return kernel_source(k, rows, coef, cse, ops);
-}
+std::string network_source(int k, int rows, const uint8_t* coef, int* ops) { return kernel_source(k, rows, coef, ops); }
 
 namespace {
 // The translation unit hipRTC compiles for one pass, and the kernel's name expression.
@@ -397,10 +413,7 @@ void unit(int k, int rows, Mode mode, bool strided, const uint8_t* coef, std::st
           int* ops) {
     const int imode = static_cast<int>(mode), addr = strided ? 0 : 1;
     *u = network_u(k, rows, imode);
-    const long wpe = tune::get(tune::kRtcWpe);
-    *src = (wpe > 0 ? "#define BLBRS_NET_WPE " + std::to_string(wpe) + "\n" : std::string()) +
-           "#define BLBRS_CM_ROW_STORES " + std::to_string(tune::get(tune::kRtcRowStores) != 0 ? 1 : 0) + "\n" +
-           "#include \"rs_code.hpp\"\n" + kernel_source(k, rows, coef, tune::get(tune::kRtcCse) != 0, ops);
+    *src = "#include \"rs_code.hpp\"\n" + kernel_source(k, rows, coef, ops);
     *name = "blbrs::code::rs_code_kernel<" + std::to_string(k) + ", " + std::to_string(rows) + ", " +
             std::to_string(imode) + ", " + std::to_string(addr) + ", " + std::to_string(*u) + ", 3, BlbrsNet>";
     *src += "// " + *name + "\n";
@@ -440,11 +453,16 @@ bool compile_only(int k, int rows, Mode mode, bool strided, const uint8_t* coef,
 
 NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const uint8_t* coef) {
     if (!eligible(k, rows)) return nullptr;
+    State& s = S();
+    {
+        // Past the cap, before building a source of up to ~30 KB that could not be used anyway.
+        std::lock_guard<std::mutex> g(s.mu);
+        if (s.kernels.size() >= kMaxEntries) return disabled();
+    }
     std::string src, name;
     int u = 0, ops = 0;
     unit(k, rows, mode, strided, coef, &src, &name, &u, &ops);
     const std::string key = std::to_string(device) + "|" + src;
-    State& s = S();
     exit_hook();
     NetKernel* nk = nullptr;
     bool sync = false;
@@ -452,7 +470,8 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
         std::lock_guard<std::mutex> g(s.mu);
         auto it = s.kernels.find(key);
         if (it != s.kernels.end()) return it->second.get();
-        if (s.exiting || s.kernels.size() >= kMaxEntries) return nullptr;
+        if (s.exiting) return nullptr;
+        if (s.kernels.size() >= kMaxEntries) return disabled();
         auto p = std::make_unique<NetKernel>();
         p->device = device;
         p->u = u;

@@ -5,24 +5,24 @@
 // P * inv(M[valid]) for missing parity -- depend on which shards are present, i.e. on the
 // erasure pattern of the call (klauspost reedsolomon.go reconstruct; blb's recovery RPC
 // rebuilds every absent slot, internal/tractserver/store.go:1062-1102).  On wide shapes the
-// v_perm table multiply is VALU-bound there too, so for such a pass this module generates the
-// pass's network as straight-line code (XOR terms shared between output planes where that saves
-// instructions), compiles rs_code_kernel<K, MR, MODE, ADDR, U, NT, Net> (rs_code.hpp) with hipRTC
+// v_perm table multiply is VALU-bound there too, so for such a pass this module can generate the
+// pass's network as straight-line code, compile rs_code_kernel<K, MR, MODE, ADDR, U, NT, Net> (rs_code.hpp) with hipRTC
 // against the library's own device headers, and loads it on the device.  The device plan caches
 // the kernel next to the pass's tables -- the counterpart of klauspost's inversion tree, one
 // level further: a compiled kernel per cached inverse.
 //
-// Compilation runs on a background thread by default (knob BLBRS_RTC = 1): the pass keeps the
-// table kernel until its network is compiled, so no call waits on the compiler.  That thread
-// makes no HIP call: hipRTC is host-only, and the code object is loaded (hipModuleLoadData) by
-// the next launch that wants it, in the launching thread (ready()).  A background module load
-// racing the library's other threads was followed by illegal-address faults in the GPU suite
-// (DESIGN §4h), so HIP work stays on the threads that own the streams.  Compiles and loads
-// share one lock (comgr, i.e. LLVM, runs in this process), a launch never waits for it, and the
-// compiler thread lives for the whole process and is joined at exit, before comgr's static
-// destructors run.  BLBRS_RTC = 2 compiles and loads in the calling thread on first use, 0
-// disables run-time networks.  A compile or load failure leaves the pass on tables (counted in
-// blbrs_rtc_get_stats).
+// Off by default (knob BLBRS_RTC = 0, round 5): the gain is RS(12,5)-wide recovery passes only
+// (2-5 % in the driver's bench), and a run-time compiler brings LLVM into blb's tractserver and
+// client processes; an illegal-address fault seen twice in round 4 while modules were loaded off
+// the launching thread has no pinned cause.  hipRTC is opened with dlopen on the
+// first request, never linked, so a process that does not opt in never maps it or comgr.
+// BLBRS_RTC = 1 compiles on a background thread: the pass keeps the table kernel until its
+// network is compiled, so no call waits on the compiler.  That thread makes no HIP call (hipRTC
+// is host-only); the code object is loaded (hipModuleLoadData) by the next launch that wants it,
+// in the launching thread (ready()).  Compiles and loads share one lock, a launch never waits for
+// it, and the compiler thread lives for the whole process and is joined at exit, before comgr's
+// static destructors run.  BLBRS_RTC = 2 compiles and loads in the calling thread on first use.
+// A compile or load failure (or hipRTC missing) leaves the pass on tables (blbrs_rtc_get_stats).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -45,10 +45,10 @@ struct NetKernel {
     int ops = 0;                             // VALU ops of the generated network per 8-dword group
 };
 
-// Per-pass lookup cache (mode x addressing), kept in the device plan.
+// Per-pass lookup cache (mode x addressing), kept in the device plan.  The generated source
+// depends on nothing but the pass (no knob shapes it), so an entry never goes stale.
 struct NetSlot {
     std::atomic<NetKernel*> k[3][2] = {};
-    std::atomic<unsigned> gen[3][2] = {};  // tune::generation() the entry was resolved under
 };
 
 // Whether a pass of `rows` rows over `k` inputs may take a run-time network (the knob
@@ -57,7 +57,8 @@ bool eligible(int k, int rows);
 
 // The network kernel for (device, rows x k coefficients, mode, addressing), requesting its
 // compilation on first use.  Returns nullptr when not eligible; otherwise an entry that stays
-// valid for the life of the process (fn == nullptr until it is ready).
+// valid for the life of the process (fn == nullptr until it is ready; a shared entry that never
+// becomes ready once the process holds kMaxEntries kernels).
 NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const uint8_t* coef);
 
 // The loaded kernel of `nk`, loading its compiled code object on nk->device in the calling thread
@@ -66,7 +67,7 @@ NetKernel* request(int device, int k, int rows, Mode mode, bool strided, const u
 hipFunction_t ready(NetKernel* nk, bool wait = false);
 
 // The generated network's source for rows x k coefficients (tests, tools).
-std::string network_source(int k, int rows, const uint8_t* coef, bool cse, int* ops);
+std::string network_source(int k, int rows, const uint8_t* coef, int* ops);
 
 // Compiles the kernel request() would build, without loading it (no device needed); true on
 // success, else false with the compiler log.  Adds to the compile cache.

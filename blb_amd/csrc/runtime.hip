@@ -331,6 +331,72 @@ bool device_view(const void* p, uint64_t* view, int* owner) {
 }
 
 // ---------------------------------------------------------------------------------------
+// pointer-table check
+// ---------------------------------------------------------------------------------------
+
+namespace {
+std::atomic<uint32_t> g_tag{0};
+std::atomic<int> g_corrupt_slot{-1};
+std::mutex g_fault_mu;
+std::map<int, uint32_t*> g_dev_fault;  // process lifetime
+}  // namespace
+
+uint32_t next_table_tag() {
+    for (;;) {
+        const uint32_t t = g_tag.fetch_add(1, std::memory_order_relaxed) & 0xFFFFu;
+        if (t) return t;
+    }
+}
+
+int tag_entries(const uint64_t* ptrs, size_t count, uint32_t tag, uint64_t* out, bool* aligned) {
+    bool al = true;
+    for (size_t i = 0; i < count; ++i) {
+        if (ptrs[i] > kPtrMask)
+            return fail(BLBRS_ERR_INVALID_ARG, "shard address above the 48-bit address space (entry " + std::to_string(i) + ")");
+        out[i] = ptrs[i] | static_cast<uint64_t>(tag) << kPtrTagShift;
+        al = al && aligned16(ptrs[i]);
+    }
+    if (const int c = g_corrupt_slot.exchange(-1); c >= 0 && static_cast<size_t>(c) < count)
+        out[c] = ptrs[c] | static_cast<uint64_t>(tag ^ 0x5A5Au) << kPtrTagShift;
+    *aligned = al;
+    return BLBRS_OK;
+}
+
+void corrupt_next_table(int slot) { g_corrupt_slot.store(slot); }
+
+int alloc_fault_record(uint32_t** out) {
+    *out = nullptr;
+    void* p = nullptr;
+    BLBRS_HIP_TRY(hipHostMalloc(&p, kFaultWords * 4, hipHostMallocDefault));
+    std::memset(p, 0, kFaultWords * 4);
+    *out = static_cast<uint32_t*>(p);
+    return BLBRS_OK;
+}
+
+uint32_t* device_fault_record(int dev) {
+    std::lock_guard<std::mutex> g(g_fault_mu);
+    uint32_t*& r = g_dev_fault[dev];
+    if (!r && alloc_fault_record(&r) != BLBRS_OK) r = nullptr;
+    return r;
+}
+
+int check_fault(uint32_t* rec, const char* what) {
+    if (!rec) return BLBRS_OK;
+    volatile uint32_t* v = rec;
+    if (!v[0]) return BLBRS_OK;
+    const uint64_t e = (static_cast<uint64_t>(v[5]) << 32) | v[4];
+    const std::string msg = std::string(what) + ": pointer table entry of stripe " + std::to_string(v[1]) + " slot " +
+                            std::to_string(v[2]) + " holds 0x" + [&] {
+                                char b[32];
+                                std::snprintf(b, sizeof b, "%016llx", static_cast<unsigned long long>(e));
+                                return std::string(b);
+                            }() + " (tag " + std::to_string(e >> kPtrTagShift) + ", launch tag " + std::to_string(v[3]) +
+                            "); the stripe was not coded";
+    for (int i = 0; i < kFaultWords; ++i) v[i] = 0;
+    return fail(BLBRS_ERR_HIP, msg);
+}
+
+// ---------------------------------------------------------------------------------------
 // stream workers
 // ---------------------------------------------------------------------------------------
 
@@ -346,7 +412,8 @@ int Worker::ensure_stage(size_t bytes) {
     return BLBRS_OK;
 }
 
-int Worker::upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned) {
+int Worker::upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned,
+                         uint32_t* tag) {
     if (count > tab_cap) {
         // The previous copy out of tab_host has completed: every call that used it ended with
         // a sync of s[0].
@@ -360,14 +427,10 @@ int Worker::upload_table(const uint64_t* ptrs, size_t count, const uint64_t** de
         BLBRS_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&tab_dev), cap * 8));
         tab_cap = cap;
     }
-    bool al = true;
-    for (size_t i = 0; i < count; ++i) {
-        tab_host[i] = ptrs[i];
-        al = al && aligned16(ptrs[i]);
-    }
+    *tag = next_table_tag();
+    if (int rc = tag_entries(ptrs, count, *tag, tab_host, aligned)) return rc;
     BLBRS_HIP_TRY(hipMemcpyAsync(tab_dev, tab_host, count * 8, hipMemcpyHostToDevice, s[0]));
     *dev_out = tab_dev;
-    *aligned = al;
     return BLBRS_OK;
 }
 
@@ -382,7 +445,9 @@ void Worker::destroy() {
     if (stage) (void)hipFree(stage);
     if (tab_host) (void)hipHostFree(tab_host);
     if (tab_dev) (void)hipFree(tab_dev);
+    if (fault) (void)hipHostFree(fault);
     stage_add(device, -static_cast<int64_t>(stage_cap));
+    fault = nullptr;
     flag = nullptr;
     stage = nullptr;
     tab_host = nullptr;
@@ -421,6 +486,7 @@ int make_worker(int dev, Worker** out) {
     for (auto& x : w->s)
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&w->flag, sizeof(int32_t));
+    if (e == hipSuccess && alloc_fault_record(&w->fault) != BLBRS_OK) e = hipErrorOutOfMemory;
     if (e != hipSuccess) {
         w->destroy();
         delete w;
@@ -566,7 +632,7 @@ PtrLease::~PtrLease() {
 }
 
 int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, const uint64_t** dev_out,
-                     bool* aligned) {
+                     bool* aligned, uint32_t* tag) {
     int dev = 0;
     BLBRS_HIP_TRY(hipGetDevice(&dev));
     SlotRing& r = ring_of(dev);
@@ -600,16 +666,24 @@ int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, con
         }
         s.cap = cap;
     }
-    bool al = true;
-    for (size_t i = 0; i < count; ++i) {
-        s.host[i] = ptrs[i];
-        al = al && aligned16(ptrs[i]);
+    if (tag) {
+        *tag = next_table_tag();
+        if (int rc = tag_entries(ptrs, count, *tag, s.host, aligned)) {
+            s.mu.unlock();
+            return rc;
+        }
+    } else {
+        bool al = true;
+        for (size_t i = 0; i < count; ++i) {
+            s.host[i] = ptrs[i];
+            al = al && aligned16(ptrs[i]);
+        }
+        *aligned = al;
     }
     slot_ = &s;
     stream_ = stream;
     BLBRS_HIP_TRY(hipMemcpyAsync(s.dev, s.host, count * 8, hipMemcpyHostToDevice, stream));
     *dev_out = s.dev;
-    *aligned = al;
     return BLBRS_OK;
 }
 

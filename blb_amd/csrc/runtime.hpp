@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/blb_rs.h"
+#include "rs_kernels.hpp"
 
 namespace blbrs {
 namespace rt {
@@ -118,6 +119,32 @@ bool zero_copy_policy(int dev, int written, int touched);
 // *owner = the device holding device memory, -1 for host memory.
 bool device_view(const void* p, uint64_t* view, int* owner = nullptr);
 
+// ---- pointer-table check (rs_code.hpp stripe_table_ok) ----
+//
+// Every shard-pointer table the library uploads is tagged: entry = address | tag << 48, with a
+// 16-bit tag drawn per upload.  The coding kernel compares each entry it is about to use with the
+// tag of ITS launch; a stripe with a wrong entry -- one left over from another call, or not an
+// address the host wrote at all -- is skipped instead of dereferenced, and the first such entry
+// is recorded in a pinned, device-mapped record of the table's owner (worker, batcher lane, or
+// the device's record for tables on caller streams).  The host reads the record after the call's
+// sync: free when clear, a named error when not.  Round 4 saw two illegal-address faults whose
+// cause inside the runtime stayed unpinned; a stale or foreign table entry is now
+// reported instead of faulting the GPU.
+constexpr int kFaultWords = 8;  // valid, stripe, slot, expected tag, entry lo, entry hi, -, -
+uint32_t next_table_tag();      // 1 .. 0xFFFF, cycling
+// out[i] = ptrs[i] | tag << 48; INVALID_ARG for an address at or above 2^48.  *aligned: every
+// address 16-byte aligned.
+int tag_entries(const uint64_t* ptrs, size_t count, uint32_t tag, uint64_t* out, bool* aligned);
+// A zeroed pinned record mapped for every device.
+int alloc_fault_record(uint32_t** out);
+// Process-wide record of `dev` (tables on caller streams: the *_ptrs entry points).
+uint32_t* device_fault_record(int dev);
+// BLBRS_OK when `rec` is clear; else clears it and fails with BLBRS_ERR_HIP naming the entry.
+int check_fault(uint32_t* rec, const char* what);
+// Test hook (blbrs_debug_corrupt_next_table): the next tagged upload writes entry `slot` with a
+// wrong tag (its address intact).
+void corrupt_next_table(int slot);
+
 // ---- stream workers ----
 
 // Staging budget per worker ring slot: k+m shards x chunk bytes fit in it.
@@ -132,9 +159,10 @@ struct Worker {
     uint64_t* tab_host = nullptr;   // pinned pointer table
     uint64_t* tab_dev = nullptr;
     size_t tab_cap = 0;             // entries
+    uint32_t* fault = nullptr;      // pinned record of the worker's table checks
     int ensure_stage(size_t bytes);
-    // Copies `count` device addresses to the worker's device table on stream s[0].
-    int upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned);
+    // Copies `count` device addresses, tagged (*tag), to the worker's device table on stream s[0].
+    int upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned, uint32_t* tag);
     void destroy();
 };
 
@@ -170,8 +198,9 @@ class PtrLease {
     PtrLease& operator=(const PtrLease&) = delete;
     ~PtrLease();
     // Uploads on `stream` (current device); the slot stays busy until the stream has run the
-    // kernels that read it.
-    int upload(const uint64_t* ptrs, size_t count, hipStream_t stream, const uint64_t** dev_out, bool* aligned);
+    // kernels that read it.  With `tag`, a shard-pointer table: entries tagged (*tag set).
+    int upload(const uint64_t* ptrs, size_t count, hipStream_t stream, const uint64_t** dev_out, bool* aligned,
+               uint32_t* tag = nullptr);
 
  private:
     PtrSlot* slot_ = nullptr;

@@ -17,10 +17,7 @@ struct Def {
 };
 // Order = enum Knob.
 constexpr Def kDefs[kCount] = {
-    {"BLBRS_BITSLICE", 1}, {"BLBRS_OCC_LDS", 0},       {"BLBRS_OCC_LDS_ECT", 0}, {"BLBRS_PACK_VARIANT", -1},
-    {"BLBRS_PE_CM_WIDE", 1}, {"BLBRS_HOST_ZC", -1},    {"BLBRS_EC_PERSISTENT", 0}, {"BLBRS_EC_FLAGS", 0},
-    {"BLBRS_RTC", 1},      {"BLBRS_RTC_CSE", 0},       {"BLBRS_RTC_WIDE", 13},      {"BLBRS_RTC_ENCODE", 0},
-    {"BLBRS_RTC_WPE", 0},     {"BLBRS_RTC_ROW_STORES", 1},
+    {"BLBRS_BITSLICE", 1}, {"BLBRS_HOST_ZC", -1}, {"BLBRS_EC_PERSISTENT", 0}, {"BLBRS_RTC", 0}, {"BLBRS_RTC_WIDE", 13},
 };
 
 // The environment is read once, here (thread-safe static initialisation).
@@ -54,17 +51,10 @@ int index_of(const char* name) {
 
 long get(Knob k) { return store().v[k].load(std::memory_order_relaxed); }
 
-namespace {
-std::atomic<unsigned> g_generation{1};
-}
-
-unsigned generation() { return g_generation.load(std::memory_order_acquire); }
-
 bool set(const char* name, long value) {
     const int i = index_of(name);
     if (i < 0) return false;
     store().v[i].store(value, std::memory_order_relaxed);
-    g_generation.fetch_add(1, std::memory_order_acq_rel);
     return true;
 }
 

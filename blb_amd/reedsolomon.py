@@ -647,6 +647,19 @@ def use_knobs(env: dict) -> None:
         set_tuning(name, int(value))
 
 
+def table_fault_take(device: int = 0):
+    """The recorded pointer-table fault of `device`'s asynchronous *_dev_ptrs calls (read and
+    cleared; synchronize the stream first), or None.  blbrs_table_fault_take."""
+    out, found = _lib.TableFault(), ctypes.c_int(0)
+    _check(_lib.load().blbrs_table_fault_take(int(device), ctypes.byref(out), ctypes.byref(found)))
+    return {f: int(getattr(out, f)) for f, _ in out._fields_} if found.value else None
+
+
+def debug_corrupt_next_table(slot: int) -> None:
+    """Test hook: the next tagged pointer-table upload carries a wrong tag in entry `slot`."""
+    _check(_lib.load().blbrs_debug_corrupt_next_table(int(slot)))
+
+
 def rtc_stats() -> dict:
     st = _lib.RtcStats()
     _check(_lib.load().blbrs_rtc_get_stats(ctypes.byref(st)))
@@ -670,14 +683,14 @@ def rtc_eligible(k: int, rows: int) -> bool:
             and 2 <= rows <= 8 and k + rows > get_tuning("BLBRS_RTC_WIDE"))
 
 
-def rtc_network_source(coef: np.ndarray, cse: bool = True) -> tuple[str, int]:
+def rtc_network_source(coef: np.ndarray) -> tuple[str, int]:
     """(device source, VALU ops per 8-dword group) of the network for a rows x k coefficient
     matrix."""
     c = np.ascontiguousarray(coef, dtype=np.uint8)
     rows, k = c.shape
     buf = ctypes.create_string_buffer(1 << 20)
     ops = ctypes.c_int(0)
-    _check(_lib.load().blbrs_rtc_network_source(k, rows, c.ctypes.data, int(cse), buf, len(buf), ctypes.byref(ops)))
+    _check(_lib.load().blbrs_rtc_network_source(k, rows, c.ctypes.data, buf, len(buf), ctypes.byref(ops)))
     return buf.value.decode(), int(ops.value)
 
 

@@ -278,6 +278,25 @@ int blbrs_get_device_stats(int device, blbrs_device_stats* out);
 /* Frees idle stream workers and idle pooled buffers. */
 int blbrs_trim(void);
 
+/* ---- pointer-table check ----
+ * Every shard-pointer table the library uploads carries a 16-bit tag per upload in bits 48-63
+ * of each entry, and the coding kernel skips (never dereferences) a stripe holding an entry
+ * without its launch's tag.  Host calls and batched calls fail with BLBRS_ERR_HIP naming the
+ * stripe, slot and entry.  The asynchronous *_dev_ptrs calls record it per device: after
+ * synchronizing the stream, blbrs_table_fault_take reads and clears that record (*found = 0
+ * when clear). */
+typedef struct {
+    uint32_t stripe;        /* stripe index within the launch */
+    uint32_t slot;          /* shard slot within the stripe */
+    uint32_t launch_tag;    /* the tag the kernel expected */
+    uint32_t entry_tag;     /* the tag the entry carried */
+    uint64_t address;       /* the entry's address bits */
+} blbrs_table_fault;
+int blbrs_table_fault_take(int device, blbrs_table_fault* out, int* found);
+/* Test hook: the next tagged table upload writes entry `slot` with a wrong tag (address
+ * intact), so the check above can be exercised without a bad address. */
+int blbrs_debug_corrupt_next_table(int slot);
+
 /* ---- CRC-32C (Castagnoli) of shard blocks ----
  * blb checksums every shard it writes on this path: ChecksumFile blocks of 65532 data
  * bytes (pkg/disk/checksum_block.go:18-34,70-80) and bulk RPC frames (pkg/rpc/
@@ -422,21 +441,20 @@ int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t s
 
 /* ---- A/B knobs and run-time networks ---- */
 
-/* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_OCC_LDS, BLBRS_OCC_LDS_ECT,
- * BLBRS_PACK_VARIANT, BLBRS_PE_CM_WIDE, BLBRS_HOST_ZC, BLBRS_EC_PERSISTENT, BLBRS_EC_FLAGS,
- * BLBRS_RTC, BLBRS_RTC_CSE, BLBRS_RTC_WIDE, BLBRS_RTC_ENCODE, BLBRS_RTC_WPE,
- * BLBRS_RTC_ROW_STORES; blb_amd/csrc/tuning.hpp) start from the environment, read
- * once, and change only here -- never by setenv while the library runs.  INVALID_ARG for an
- * unknown name. */
+/* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_HOST_ZC, BLBRS_EC_PERSISTENT, BLBRS_RTC,
+ * BLBRS_RTC_WIDE; blb_amd/csrc/tuning.hpp), each a choice between shipped policies,
+ * start from the environment, read once, and change only here -- never by setenv while the
+ * library runs.  INVALID_ARG for an unknown name. */
 int blbrs_set_tuning(const char* name, long value);
 int blbrs_get_tuning(const char* name, long* value);
 
 /* Decode networks generated per erasure pattern and compiled with hipRTC.
- * A wide decode pass (k + rows > BLBRS_RTC_WIDE) requests its network on first use; with
- * BLBRS_RTC = 1 (default) it compiles in the background (a host-only thread, no HIP call) and the
- * pass runs the table kernel until the network is compiled; the next launch of the pass then
- * loads the code object in its own thread.  With BLBRS_RTC = 2 the first call compiles and loads
- * it, 0 disables them. */
+ * Off by default (BLBRS_RTC = 0): the library does not link hipRTC and opens it (dlopen) only
+ * when a network is first requested.  With BLBRS_RTC = 1 a wide decode pass
+ * (k + rows > BLBRS_RTC_WIDE) requests its network on first use; it compiles in the background (a
+ * host-only thread, no HIP call) and the pass runs the table kernel until the network is compiled;
+ * the next launch of the pass then loads the code object in its own thread.  With BLBRS_RTC = 2
+ * the first call compiles and loads it.  hipRTC missing = a compile failure: tables. */
 typedef struct {
     uint64_t requested;  /* networks requested (one per pass, mode, addressing, device) */
     uint64_t compiled;   /* distinct sources compiled */
@@ -457,7 +475,7 @@ int blbrs_rtc_compile(int k, int rows, const uint8_t* coef, int mode, int stride
 int blbrs_rtc_wait(long timeout_ms);
 /* The generated network (device source) for rows x k coefficients, NUL-terminated into out
  * (cap bytes); *ops = its VALU ops per 8-dword group.  INVALID_ARG when cap is too small. */
-int blbrs_rtc_network_source(int k, int rows, const uint8_t* coef, int cse, char* out, size_t cap, int* ops);
+int blbrs_rtc_network_source(int k, int rows, const uint8_t* coef, char* out, size_t cap, int* ops);
 
 const char* blbrs_last_error(void);    /* thread-local message for the last failure */
 const char* blbrs_version(void);

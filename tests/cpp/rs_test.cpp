@@ -907,7 +907,7 @@ static void TestConcurrentHostSlots(T* t) {
 }
 
 // Wide recovery from many threads at once (RS(12,5), 2..5 erasures from a small set of
-// patterns): every pass with k + rows > 13 requests a run-time network, the background thread
+// patterns), run-time networks opted in: every pass with k + rows > 13 requests a network, the background thread
 // compiles it (no HIP call there), and whichever launching thread next finds it compiled loads
 // it while the others keep launching -- the interleaving rtc.hpp describes.  Shards are pool
 // buffers or pageable memory.  Every rebuilt shard is compared with the truth.
@@ -918,6 +918,9 @@ static void TestConcurrentWideRecovery(T* t) {
     if (blbrs_new(k, m, &enc) != BLBRS_OK) Fatalf("New: %s", blbrs_last_error());
     uint8_t mat[n * k];
     blbrs_matrix(enc, mat, sizeof(mat));
+    long rtc0 = 0;
+    blbrs_get_tuning("BLBRS_RTC", &rtc0);
+    blbrs_set_tuning("BLBRS_RTC", 1);  // opt in: background compiles, loads by the launching threads
     blbrs_rtc_stats st0{};
     blbrs_rtc_get_stats(&st0);
     const std::vector<std::vector<int>> patterns = {{1, 3}, {0, 5, 11}, {2, 4, 6, 8}, {1, 3, 5, 8, 10}, {12, 14}, {0, 13, 16}};
@@ -971,6 +974,7 @@ static void TestConcurrentWideRecovery(T* t) {
     for (auto& x : th) x.join();
     blbrs_rtc_stats st1{};
     blbrs_rtc_get_stats(&st1);
+    blbrs_set_tuning("BLBRS_RTC", rtc0);
     blbrs_free(enc);
     for (const auto& s : errors) t->Errorf("%s", s.c_str());
     if (st1.failed != st0.failed) t->Errorf("run-time network failures: %llu", (unsigned long long)(st1.failed - st0.failed));

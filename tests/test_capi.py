@@ -114,7 +114,7 @@ def test_compiled_network_covers_blb_classes(knob):
     all 30 shapes run the bit-plane network.  By default only the wide shapes do, each kernel
     with its own threshold (rs_code_kernel and PackTracts + Encode k + m > 9, the fused
     encode+CRC tile kernel k + m > 11); other shapes and BLBRS_BITSLICE=0 keep the v_perm
-    table path.  Wide k outside the compiled list takes a run-time network (rtc)."""
+    table path.  Wide k outside the compiled list takes a run-time network (rtc) when opted in."""
     from blb_amd import reedsolomon as rs
     knob("BLBRS_BITSLICE", 2)
     for k in (3, 4, 6, 8, 10, 12):
@@ -127,6 +127,10 @@ def test_compiled_network_covers_blb_classes(knob):
     assert [nets[s]["code"] for s in ((12, 5), (10, 4), (8, 3), (6, 3), (3, 2))] == [True, True, True, False, False]
     assert [nets[s]["tile"] for s in ((12, 5), (10, 4), (8, 3), (6, 3))] == [True, True, False, False]
     assert [nets[s]["pack"] for s in ((12, 5), (10, 4), (8, 3), (6, 3))] == [True, True, True, False]
-    assert nets[(14, 4)] == {"code": False, "tile": False, "pack": False, "rtc": True}
+    # run-time networks are off by default (BLBRS_RTC = 0); opted in, wide k outside the list takes one
+    assert nets[(14, 4)] == {"code": False, "tile": False, "pack": False, "rtc": False}
+    knob("BLBRS_RTC", 1)
+    assert rs.New(14, 4).compiled_network() == {"code": False, "tile": False, "pack": False, "rtc": True}
+    assert not rs.New(12, 5).compiled_network()["rtc"]   # the compiled encode network wins
     knob("BLBRS_BITSLICE", 0)
     assert not any(rs.New(12, 5).compiled_network().values())

@@ -156,15 +156,14 @@ def test_gpu_pack_pieces_vs_oracle(piece_len):
 
 
 @gpu
-@pytest.mark.parametrize("variant", [0, 6, 8, 10])
-def test_gpu_pack_kernel_variants_vs_oracle(knob, variant):
-    """Every pack_kernel variant (knob BLBRS_PACK_VARIANT, pack.hip) against the oracle: random
-    extents, plus regions whose 16-byte chunk count sits at the wave and workgroup edges the
-    DPP neighbour exchange depends on (0, 1, 63-65, 255-257, 1023-1025 chunks), from every
-    source misalignment 0..15 and destination offsets that leave heads and tails."""
+@pytest.mark.parametrize("seed", [0, 1])
+def test_gpu_pack_kernel_edges_vs_oracle(seed):
+    """pack_kernel (pack.hip) against the oracle: random extents, plus regions whose 16-byte
+    chunk count sits at the wave and workgroup edges the DPP neighbour exchange depends on (0, 1,
+    63-65, 255-257, 1023-1025 chunks), from every source misalignment 0..15 and destination
+    offsets that leave heads and tails."""
     torch = _torch()
-    knob("BLBRS_PACK_VARIANT", variant)
-    rng = np.random.default_rng(1000 + variant)
+    rng = np.random.default_rng(1006 + seed)
     pool = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
     dpool = torch.from_numpy(pool).cuda()
     piece_len = 1_000_003

@@ -81,13 +81,11 @@ def test_generated_network_equals_oracle(k, m, present, data_only):
     valid, rows = pass_rows(k, m, present, data_only)
     inputs = [rng.integers(0, 256, 4096, dtype=np.uint8) for _ in range(k)]
     want = N.code(rows, inputs)
-    ops = {}
-    for cse in (True, False):
-        src, ops[cse] = rs.rtc_network_source(rows, cse=cse)
-        got = eval_network(src, k, rows.shape[0], inputs)
-        for r in range(rows.shape[0]):
-            assert np.array_equal(got[r], want[r]), (k, m, cse, r)
-    assert ops[True] <= ops[False]
+    src, ops = rs.rtc_network_source(rows)
+    got = eval_network(src, k, rows.shape[0], inputs)
+    for r in range(rows.shape[0]):
+        assert np.array_equal(got[r], want[r]), (k, m, r)
+    assert ops > 0
 
 
 def test_generated_network_random_matrices():
@@ -97,7 +95,7 @@ def test_generated_network_random_matrices():
         rows = rng.integers(0, 256, (r, k), dtype=np.uint8)
         rows[0, 0] = 0  # zero coefficients and rows are legal
         inputs = [rng.integers(0, 256, 512, dtype=np.uint8) for _ in range(k)]
-        src, _ = rs.rtc_network_source(rows, cse=True)
+        src, _ = rs.rtc_network_source(rows)
         got = eval_network(src, k, r, inputs)
         want = N.code(rows, inputs)
         assert all(np.array_equal(a, b) for a, b in zip(got, want)), (k, r)
@@ -114,8 +112,7 @@ def test_network_kernel_compiles_for_gfx950():
 
 
 def test_knobs_read_once_and_settable(knob):
-    for name in ("BLBRS_BITSLICE", "BLBRS_RTC", "BLBRS_RTC_CSE", "BLBRS_RTC_WIDE", "BLBRS_HOST_ZC",
-                 "BLBRS_EC_PERSISTENT", "BLBRS_PACK_VARIANT"):
+    for name in ("BLBRS_BITSLICE", "BLBRS_RTC", "BLBRS_RTC_WIDE", "BLBRS_HOST_ZC", "BLBRS_EC_PERSISTENT"):
         v = rs.get_tuning(name)
         knob(name, v + 1)
         assert rs.get_tuning(name) == v + 1
@@ -178,6 +175,65 @@ def test_gpu_rpc_and_client_shapes_with_networks(k, m, knob):
     if k + m > 9:
         assert after["loaded"] > before["loaded"], (before, after)
         assert after["failed"] == before["failed"], rs.rtc_stats()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m", [(10, 4), (12, 5)])
+def test_gpu_network_verify_modes_flag_corruption(k, m, knob):
+    """Networks in the compare modes (opted in, BLBRS_RTC = 2, threshold 9): reconstructAndVerify
+    with e < m data pieces missing is ONE store+verify pass (MODE 2: e rows stored, the m - e
+    parity pieces the decode did not read compared), on a device batch (strided) and a host call
+    (pointer table); a corrupted leftover parity byte inside a whole tile must turn that
+    stripe's verdict false and only that one.  The network must have been loaded."""
+    torch = _torch()
+    knob("BLBRS_RTC", 2)
+    knob("BLBRS_RTC_WIDE", 9)
+    S, B = 3 * 16384 + 4 * 1000 + 16, 3
+    host = _oracle_stripes(k, m, B, S, 500 + k)
+    enc = rs.New(k, m)
+    before = rs.rtc_stats()
+    miss = [1, 4]                          # e = 2 < m: rows = 2 stored + (m - 2) compared
+    present = [i not in miss for i in range(k + m)]
+    bad = host.copy()
+    bad[1, k + m - 1, 5000] ^= 0x40        # a leftover parity piece of stripe 1, inside tile 0
+    st = torch.from_numpy(bad).cuda()
+    for i in miss:
+        st[:, i].fill_(0xA5)
+    ok = enc.ReconstructAndVerifyBatch(st, present).cpu().numpy()
+    assert list(ok) == [True, False, True], ok
+    got = st.cpu().numpy()
+    for i in miss:
+        assert np.array_equal(got[:, i], host[:, i]), i
+    for b, want in ((0, True), (1, False)):
+        sh = [bad[b, i].copy() if present[i] else None for i in range(k + m)]
+        assert enc.ReconstructAndVerify(sh) is want, b
+        for i in miss:
+            assert np.array_equal(sh[i], host[b, i]), (b, i)
+    after = rs.rtc_stats()
+    assert after["loaded"] >= before["loaded"] + 2, (before, after)   # strided and pointer-table kernels
+    assert after["failed"] == before["failed"]
+
+
+@pytest.mark.gpu
+def test_gpu_network_verify_k_outside_compiled_list(knob):
+    """Verify for k = 14 (no compiled encode network): opted in, the parity check runs on a
+    run-time network in verify mode (MODE 1); a corrupted parity byte and a corrupted data byte,
+    each inside a whole tile of its own stripe, are both flagged."""
+    torch = _torch()
+    knob("BLBRS_RTC", 2)
+    k, m = 14, 4
+    S, B = 2 * 16384 + 4 * 1000, 3
+    host = _oracle_stripes(k, m, B, S, 1404)
+    enc = rs.New(k, m)
+    assert enc.compiled_network()["rtc"]
+    before = rs.rtc_stats()
+    bad = host.copy()
+    bad[0, k + 2, 100] ^= 1                # parity
+    bad[2, 7, 20000] ^= 0x80               # data
+    ok = enc.VerifyBatch(torch.from_numpy(bad).cuda()).cpu().numpy()
+    assert list(ok) == [False, True, False], ok
+    assert rs.rtc_stats()["loaded"] > before["loaded"]
+    assert rs.rtc_stats()["failed"] == before["failed"]
 
 
 @pytest.mark.gpu

@@ -1,0 +1,188 @@
+"""The pointer-table check (runtime.hpp TableFault, rs_code.hpp stripe_table_ok) and the lazily
+opened run-time compiler (rtc.hip).
+
+Round 4 saw two hipErrorIllegalAddress faults in the GPU suite whose cause inside the runtime was
+never pinned.  Two changes answer it:
+
+* every shard-pointer table the library uploads is tagged per upload, and the coding kernel never
+  dereferences an entry without its launch's tag -- a stale or foreign entry becomes a named
+  error (stripe, slot, entry) instead of a device fault;
+* run-time decode networks are off by default and hipRTC is opened with dlopen on first use, so
+  blb's tractserver and client processes carry no in-process LLVM unless they opt in.
+
+The GPU tests inject a wrong tag (blbrs_debug_corrupt_next_table: the address stays valid, so the
+pre-check logic would have coded the stripe normally) into each path that uploads a table: host
+calls on the worker's table (zero-copy and staged), the batcher's lane table, and the caller-stream
+*_dev_ptrs table.  Each must leave the stripe untouched, report the slot, and keep the device usable.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from blb_amd import reedsolomon as rs
+from oracle import rs_numpy as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "blb_amd", "libblbrs.so")
+
+
+def _maps_after(code: str) -> str:
+    """/proc/self/maps of a fresh interpreter after `code` ran (library loaded as `lib`)."""
+    script = ("import ctypes, sys\nsys.path.insert(0, %r)\nfrom blb_amd import _lib\nlib = _lib.load()\n" % ROOT
+              + code + "\nprint(open('/proc/self/maps').read())\n")
+    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return p.stdout
+
+
+def test_library_does_not_link_hiprtc():
+    """ldd shows no hipRTC or comgr, and loading the library maps neither."""
+    out = subprocess.run(["ldd", LIB], capture_output=True, text=True, check=True).stdout
+    assert "hiprtc" not in out and "comgr" not in out, out
+    maps = _maps_after("")
+    assert "libhiprtc" not in maps
+
+
+def test_rtc_default_off():
+    assert rs.get_tuning("BLBRS_RTC") == 0
+    assert not rs.rtc_eligible(12, 5)
+
+
+def test_hiprtc_opened_on_first_compile():
+    """A compile request (no device needed) opens hipRTC lazily: mapped afterwards."""
+    maps = _maps_after("import numpy as np\nfrom blb_amd import reedsolomon as rs\n"
+                       "rs.rtc_compile(np.arange(1, 1 + 2 * 12, dtype=np.uint8).reshape(2, 12), mode=0)")
+    assert "libhiprtc" in maps
+
+
+# ---------------------------------------------------------------- GPU -------------------------
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stripe(k, m, S, seed):
+    rng = np.random.default_rng(seed)
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+    return data + list(N.encode(k, m, data))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pool", [True, False])
+def test_gpu_wrong_tag_host_call_names_slot(pool):
+    """Host Encode (pool buffers: zero copy on the worker's table; pageable: staged, per-chunk
+    tables): an entry with a wrong tag fails the call with ErrHIP naming the slot, the parity is
+    not written, and the next call on the same encoder is bit-exact."""
+    k, m, S = 6, 3, 3 * 16384 + 100
+    truth = _stripe(k, m, S, 11 + pool)
+    enc = rs.New(k, m)
+    for slot in (0, k + 1):
+        if pool:
+            sh = [rs.GetBuffer(S)[:S] for _ in range(k + m)]
+        else:
+            sh = [np.empty(S, np.uint8) for _ in range(k + m)]
+        for i in range(k):
+            sh[i][:] = truth[i]
+        for i in range(k, k + m):
+            sh[i][:] = 0xA5
+        rs.debug_corrupt_next_table(slot)
+        with pytest.raises(rs.ErrHIP, match=f"slot {slot} "):
+            enc.Encode(sh)
+        if pool:  # zero copy: the skipped stripe's parity is untouched (staged outputs are unspecified)
+            for i in range(k, k + m):
+                assert (sh[i] == 0xA5).all(), (slot, i)
+        enc.Encode(sh)
+        for i in range(k, k + m):
+            assert np.array_equal(sh[i], truth[i]), (slot, i)
+        if pool:
+            for b in sh:
+                rs.PutBuffer(b)
+
+
+@pytest.mark.gpu
+def test_gpu_wrong_tag_batched_call_names_slot():
+    """A batched ReconstructData: the lane's table check fails the group with the slot named;
+    the next batched call is bit-exact."""
+    k, m, S = 6, 3, 65536
+    truth = _stripe(k, m, S, 21)
+    enc = rs.New(k, m)
+    b = rs.Batcher(max_batch=8, window_us=0)
+    enc.SetBatcher(b)
+    try:
+        for attempt in range(2):
+            sh = [truth[i].copy() if i != 2 else None for i in range(k)] + [truth[i].copy() for i in range(k, k + m)]
+            if attempt == 0:
+                rs.debug_corrupt_next_table(4)
+                with pytest.raises(rs.ErrHIP, match="slot 4 "):
+                    enc.ReconstructData(sh)
+            else:
+                enc.ReconstructData(sh)
+                assert np.array_equal(sh[2], truth[2])
+    finally:
+        enc.SetBatcher(None)
+
+
+@pytest.mark.gpu
+def test_gpu_wrong_tag_dev_ptrs_recorded_per_device():
+    """Encode of device tensors (blbrs_encode_dev_ptrs, asynchronous on the caller's stream):
+    the stripe is skipped and the device record names the slot and both tags; taking the record
+    clears it; the device keeps working."""
+    torch = _torch()
+    k, m, S = 12, 5, 2 * 16384 + 48
+    truth = _stripe(k, m, S, 31)
+    enc = rs.New(k, m)
+    assert rs.table_fault_take(0) is None
+    sh = [torch.from_numpy(truth[i]).cuda() if i < k else torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
+          for i in range(k + m)]
+    rs.debug_corrupt_next_table(k + 2)
+    enc.Encode(sh)
+    torch.cuda.synchronize()
+    f = rs.table_fault_take(0)
+    assert f is not None and f["slot"] == k + 2 and f["stripe"] == 0, f
+    assert f["entry_tag"] != f["launch_tag"] and f["address"] == sh[k + 2].data_ptr()
+    assert rs.table_fault_take(0) is None
+    for i in range(k, k + m):
+        assert bool((sh[i] == 0xA5).all()), i
+    enc.Encode(sh)
+    torch.cuda.synchronize()
+    assert rs.table_fault_take(0) is None
+    for i in range(k, k + m):
+        assert np.array_equal(sh[i].cpu().numpy(), truth[i]), i
+
+
+@pytest.mark.gpu
+def test_gpu_default_recovery_keeps_hiprtc_out_of_the_process():
+    """blb's widest recovery shape (RS(12,5), 5 bad pieces, every absent slot rebuilt) with the
+    default knobs runs on tables and leaves hipRTC unmapped; opting in (BLBRS_RTC=2) opens it and
+    loads a network, with the same bytes."""
+    code = r'''
+import numpy as np, torch
+from blb_amd import reedsolomon as rs
+from oracle import rs_numpy as N
+k, m, S = 12, 5, 2 * 16384 + 48
+rng = np.random.default_rng(5)
+data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+host = np.stack(data + list(N.encode(k, m, data)))[None]
+present = [i not in (1, 3, 5, 8, 10) for i in range(k + m)]
+enc = rs.New(k, m)
+def run():
+    st = torch.from_numpy(host).cuda()
+    for i in range(k + m):
+        if not present[i]:
+            st[:, i].fill_(0)
+    enc.ReconstructBatch(st, present)
+    assert np.array_equal(st.cpu().numpy(), host)
+run()
+assert rs.rtc_stats()["requested"] == 0
+print("MAPS1", "libhiprtc" in open("/proc/self/maps").read())
+rs.set_tuning("BLBRS_RTC", 2)
+run()
+assert rs.rtc_stats()["loaded"] >= 1, rs.rtc_stats()
+print("MAPS2", "libhiprtc" in open("/proc/self/maps").read())
+'''
+    out = _maps_after(code)
+    assert "MAPS1 False" in out and "MAPS2 True" in out, out[-2000:]
