@@ -28,6 +28,9 @@ sys.path.insert(0, ROOT)
 from blb_amd import multigpu  # noqa: E402
 from blb_amd import reedsolomon as rs  # noqa: E402
 
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import tract_layout as TL  # noqa: E402  (synthetic PackTracts extent sets)
+
 GIB = float(1 << 30)
 TRACT = 8 * 1024 * 1024          # core.TractLength (internal/core/constants.go:15)
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -582,28 +585,24 @@ def cold_class_extras(S, dev, batch=512, reps=4):
     fc_ms = _ev_ms(lambda: e.EncodeBatchCRC(st, 65532, phase=256, seeds=seeds), reps, stream, dev)
     row("encode_crc_fused_b65532_phase256", fc_ms, batch * n * S, ratio_to_encode=round(fc_ms / enc_ms, 3),
         verify_ok=bool(e.VerifyBatch(st).all()))
-    # PackTracts + Encode: tracts of 64 KiB..8 MiB from a 4 GiB device pool at padToLength-
-    # aligned offsets into the B*k data pieces (the main bench's extent generator).
-    pool = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev)
-    prng = np.random.default_rng(83)
-    ext, read_bytes = [], 0
-    for p in range(batch * k):
-        off = 0
-        while True:
-            ln = int(prng.integers(64 << 10, (8 << 20) + 1))
-            if off + ln > S:
-                break
-            src = int(prng.integers(0, pool.numel() - ln))
-            ext.append((pool[src:], off, ln, p))
-            read_bytes += ln
-            off += pack.padded_length(ln)
-    pack.PackEncode(e, st, ext)
-    torch.cuda.synchronize(dev)
-    torch.cuda._sleep(400_000_000)  # keeps the host-side extent checks outside the window
-    pe_ms = _ev_ms(lambda: pack.PackEncode(e, st, ext), 1, stream, dev)
-    row("pack_encode_fused", pe_ms, read_bytes + batch * n * S, bytes_read=read_bytes,
-        tracts=len(ext), verify_ok=bool(e.VerifyBatch(st).all()))
-    del st, pool, ext
+    # PackTracts + Encode: tracts of 64 KiB..8 MiB at padToLength-aligned offsets into the B*k
+    # data pieces, from distinct sources (the row's rate) and from one shared 4 GiB pool
+    # (tools/tract_layout.py).
+    lay = TL.layout(batch * k, S, np.random.default_rng(83))
+    read_bytes = sum(ln for _, _, ln in lay)
+    pe = {}
+    for name, (pool, starts) in (("distinct", TL.distinct_sources(lay, dev, g, np.random.default_rng(84))),
+                                 ("shared", TL.shared_sources(lay, 4 << 30, dev, np.random.default_rng(85)))):
+        ext = TL.extents(lay, pool, starts)
+        pack.PackEncode(e, st, ext)
+        torch.cuda.synchronize(dev)
+        torch.cuda._sleep(400_000_000)  # keeps the host-side extent checks outside the window
+        pe[name] = (_ev_ms(lambda: pack.PackEncode(e, st, ext), 1, stream, dev), bool(e.VerifyBatch(st).all()))
+        del pool, ext
+    row("pack_encode_fused", pe["distinct"][0], read_bytes + batch * n * S, sources="distinct",
+        shared_pool_ms=round(pe["shared"][0], 3), bytes_read=read_bytes, tracts=len(lay),
+        verify_ok=pe["distinct"][1] and pe["shared"][1])
+    del st
     torch.cuda.empty_cache()
     return out
 
@@ -765,63 +764,65 @@ def main():
                 "kernel": "encode_crc_tile_kernel + tile_combine_kernel",
                 "persistent_segment_kernel_ms": round(p_ms, 3),
                 "separate_encode_plus_crc_ms": round(launch_ms + crc_ms, 3) if blk else None}
-        # PackTracts (§8f row 3): lay tracts of random length (64 KiB..8 MiB, from a 4 GiB
-        # device pool) at padToLength-aligned offsets into the B*k data pieces, zero-filling
-        # holes and tails.  HBM bytes = tract bytes read + piece bytes written.
+        # PackTracts (§8f row 3): lay tracts of random length (64 KiB..8 MiB) at padToLength-
+        # aligned offsets into the B*k data pieces, zero-filling holes and tails.  HBM bytes =
+        # tract bytes read + piece bytes written.  Timed on two source sets over one layout
+        # (tools/tract_layout.py): DISTINCT (every tract its own bytes -- the headline rate, every
+        # byte read is a distinct HBM byte) and SHARED (windows of one 4 GiB pool, rounds 2-4;
+        # overlapping windows can be served by L2 / MALL).
         from blb_amd import pack
-        pool = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev)
-        prng = np.random.default_rng(17)
-        per_col = []
-        read_bytes = 0
-        for j in range(k):
-            ext = []
-            for b in range(B):
-                off = 0
-                while True:
-                    ln = int(prng.integers(64 << 10, (8 << 20) + 1))
-                    if off + ln > S:
-                        break
-                    src = int(prng.integers(0, pool.numel() - ln))
-                    ext.append((pool[src:], off, ln, b))
-                    read_bytes += ln
-                    off += pack.padded_length(ln)
-            per_col.append(ext)
+        lay = TL.layout(B * k, S, np.random.default_rng(17))  # piece p = stripe p // k, shard p % k
+        read_bytes = sum(ln for _, _, ln in lay)
+        srcs = {"distinct": TL.distinct_sources(lay, dev, g, np.random.default_rng(18)),
+                "shared": TL.shared_sources(lay, 4 << 30, dev, np.random.default_rng(19))}
         cols = [stripes[:, j, :] for j in range(k)]
-        for j in range(k):
-            pack.PackPieces(cols[j], S, per_col[j])
-        torch.cuda.synchronize(dev)
-        pk_evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        torch.cuda._sleep(400_000_000)  # keeps the host-side extent checks outside the window
-        pk_evs[0].record(stream)
-        for j in range(k):
-            pack.PackPieces(cols[j], S, per_col[j])
-        pk_evs[1].record(stream)
-        torch.cuda.synchronize(dev)
-        pk_ms = pk_evs[0].elapsed_time(pk_evs[1])
+
+        def pack_ms(pool, starts):
+            ext = TL.extents(lay, pool, starts)
+            per_col = [[(src, off, ln, p // k) for (src, off, ln, p) in ext if p % k == j] for j in range(k)]
+            for j in range(k):
+                pack.PackPieces(cols[j], S, per_col[j])
+            torch.cuda.synchronize(dev)
+            evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            torch.cuda._sleep(400_000_000)  # keeps the host-side extent checks outside the window
+            evs[0].record(stream)
+            for j in range(k):
+                pack.PackPieces(cols[j], S, per_col[j])
+            evs[1].record(stream)
+            torch.cuda.synchronize(dev)
+            return evs[0].elapsed_time(evs[1])
+
+        def pack_encode_ms(pool, starts):
+            # PackTracts fused with Encode (curator encPack -> encEncode in one pass): piece
+            # b*k + j is data shard j of stripe b; parity encoded from registers.
+            ext = TL.extents(lay, pool, starts)
+            pack.PackEncode(enc, stripes, ext)
+            torch.cuda.synchronize(dev)
+            evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            torch.cuda._sleep(400_000_000)
+            evs[0].record(stream)
+            pack.PackEncode(enc, stripes, ext)
+            evs[1].record(stream)
+            torch.cuda.synchronize(dev)
+            return evs[0].elapsed_time(evs[1]), bool(enc.VerifyBatch(stripes).all())
+
+        pk = {name: pack_ms(*v) for name, v in srcs.items()}
+        pe = {name: pack_encode_ms(*v) for name, v in srcs.items()}
         pk_bytes = read_bytes + B * k * S
-        extra["pack_tracts"] = {"hbm_GBps": round(pk_bytes / (pk_ms * 1e-3) / 1e9, 1), "ms": round(pk_ms, 3),
-                                "pieces": B * k, "tracts": sum(len(e) for e in per_col),
-                                "bytes_read": read_bytes, "bytes_written": B * k * S}
-        # PackTracts fused with Encode (curator encPack -> encEncode in one pass): the same
-        # extents as data shard j of stripe b = piece b*k + j; parity encoded from registers.
-        fused_ext = sorted(((src, off, ln, b * k + j) for j in range(k) for (src, off, ln, b) in per_col[j]),
-                           key=lambda x: (x[3], x[1]))
-        pack.PackEncode(enc, stripes, fused_ext)
-        torch.cuda.synchronize(dev)
-        fe_evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        torch.cuda._sleep(400_000_000)
-        fe_evs[0].record(stream)
-        pack.PackEncode(enc, stripes, fused_ext)
-        fe_evs[1].record(stream)
-        torch.cuda.synchronize(dev)
-        fe_ms = fe_evs[0].elapsed_time(fe_evs[1])
-        fe_ok = bool(enc.VerifyBatch(stripes).all())
         fe_bytes = read_bytes + B * (k + m) * S
-        extra["pack_encode_fused"] = {"ms": round(fe_ms, 3), "hbm_GBps": round(fe_bytes / (fe_ms * 1e-3) / 1e9, 1),
-                                      "separate_pack_plus_encode_ms": round(pk_ms + launch_ms, 3),
+        extra["pack_tracts"] = {"sources": "distinct", "ms": round(pk["distinct"], 3),
+                                "hbm_GBps": round(pk_bytes / (pk["distinct"] * 1e-3) / 1e9, 1),
+                                "frac_of_8TBps": round(pk_bytes / (pk["distinct"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "shared_pool_ms": round(pk["shared"], 3),
+                                "pieces": B * k, "tracts": len(lay), "bytes_read": read_bytes, "bytes_written": B * k * S}
+        extra["pack_encode_fused"] = {"sources": "distinct", "ms": round(pe["distinct"][0], 3),
+                                      "hbm_GBps": round(fe_bytes / (pe["distinct"][0] * 1e-3) / 1e9, 1),
+                                      "frac_of_8TBps": round(fe_bytes / (pe["distinct"][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "shared_pool_ms": round(pe["shared"][0], 3),
+                                      "separate_pack_plus_encode_ms": round(pk["distinct"] + launch_ms, 3),
                                       "bytes_read": read_bytes, "bytes_written": B * (k + m) * S,
-                                      "verify_ok": fe_ok, "kernel": "pack_encode_kernel"}
-        del pool, per_col
+                                      "verify_ok": pe["distinct"][1] and pe["shared"][1], "kernel": "pack_encode_kernel"}
+        del srcs, cols
 
     if not a.no_extra and a.shard == TRACT:
         del stripes

@@ -7,6 +7,7 @@ used only to line the ranks up (barrier) and to take the max-over-ranks wall tim
 from __future__ import annotations
 
 import os
+import platform
 from dataclasses import dataclass
 
 
@@ -104,14 +105,31 @@ def bind_to_node(node: int, sysfs: str = "/sys/devices/system/node") -> dict:
     mine = os.sched_getaffinity(0)
     both = cpus & mine
     if both:
-        os.sched_setaffinity(0, both)
+        # sched_setaffinity(0) binds only the calling thread: bind every thread the process
+        # already has (the HIP runtime's among them), and the caller's future threads inherit it.
+        for tid in _threads():
+            try:
+                os.sched_setaffinity(tid, both)
+            except OSError:
+                pass  # the thread ended meanwhile
         out["cpus_bound"] = len(both)
     else:
         out["reason"] = "node's CPUs outside this job's affinity"
     mask = ctypes.c_ulong(1 << node) if node < 64 else None
+    if platform.machine() != "x86_64":
+        mask = None  # the syscall number is x86_64's (238 is migrate_pages on aarch64)
+        out["mempolicy"] = f"skipped on {platform.machine()}"
     if mask is not None:
         libc = ctypes.CDLL(None, use_errno=True)
         rc = libc.syscall(_SYS_SET_MEMPOLICY, _MPOL_PREFERRED, ctypes.byref(mask), ctypes.c_ulong(64))
         out["mempolicy"] = "preferred" if rc == 0 else f"failed errno {ctypes.get_errno()}"
     out["bound"] = bool(both) and out["mempolicy"] == "preferred"
     return out
+
+
+def _threads() -> list:
+    """Thread ids of this process (/proc/self/task), the calling thread when unreadable."""
+    try:
+        return [int(t) for t in os.listdir("/proc/self/task")]
+    except OSError:
+        return [0]

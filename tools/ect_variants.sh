@@ -24,6 +24,6 @@ for spec in "$@"; do
     b=$(basename $o .o)
     if [ -f $out/obj/$b.o ]; then objs="$objs $out/obj/$b.o"; else objs="$objs $o"; fi
   done
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $out/libblbrs.so $objs -lhiprtc
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $out/libblbrs.so $objs -ldl
   rm -rf $out/obj
 done

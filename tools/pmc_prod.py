@@ -14,6 +14,8 @@ the same process:
   encode_crc_65532  EncodeBatchCRC(65532)                         (encode_crc_tile_kernel + combine)
   crc32c_65532      ChecksumBatch of parity shard k, 65532 blocks (crc_stream_kernel)
   pack_tracts       PackPieces of B 8 MiB pieces from distinct tract sources (pack_kernel)
+  pack_encode_rs6_3_distinct  PackEncode of all B*k data pieces, distinct sources (pack_encode_kernel)
+  pack_encode_rs8_3_distinct  the same at RS(8,3) B=512
   then RS(12,5) B=512: EncodeBatch and EncodeBatchCRC(65532) on the compiled network, a
   VerifyBatch, and blb's recovery RPC shape (data shard 1 bad, the first 12 good pieces read,
   all 5 absent slots rebuilt) on its run-time network (BLBRS_RTC = 2: compiled by the warm-up).
@@ -33,6 +35,8 @@ sys.path.insert(0, ROOT)
 from blb_amd import _lib  # noqa: E402
 from blb_amd import checksum, pack  # noqa: E402
 from blb_amd import reedsolomon as rs  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import tract_layout as TL  # noqa: E402
 
 REPS = int(os.environ.get("PMC_REPS", "3"))
 k, m, B, S = 6, 3, 1024, 8 << 20
@@ -47,6 +51,14 @@ def op(label, needle, fn, algo, **extra):
         fn()
         torch.cuda.synchronize()
     plan.append({"label": label, "needle": needle, "launches": 1 + REPS, "algorithmic_bytes": algo, **extra})
+
+
+def check(label, needle, fn):
+    """One untimed launch the summary steps over (a verification between ops)."""
+    r = fn()
+    torch.cuda.synchronize()
+    plan.append({"label": label, "needle": needle, "launches": 1, "skip": True, "algorithmic_bytes": 0})
+    return r
 
 
 src = torch.empty(8 << 30, dtype=torch.uint8, device=dev)
@@ -74,31 +86,48 @@ op("encode_crc_65532", "encode_crc_tile_kernel", lambda: enc.EncodeBatchCRC(st, 
 op("crc32c_65532", "crc_stream_kernel", lambda: checksum.ChecksumBatch(st[:, k], 65532), B * S)
 # PackTracts into data shard 0 of every stripe (B pieces of 8 MiB): tracts of 64 KiB..8 MiB at
 # padToLength offsets, every tract its own source bytes (end to end in a shuffled order, so
-# no read is served by another tract's cached lines).
+# no read is served by another tract's cached lines; tools/tract_layout.py).
 prng = np.random.default_rng(17)
-layout = []
-for b in range(B):
-    off = 0
-    while True:
-        ln = int(prng.integers(64 << 10, (8 << 20) + 1))
-        if off + ln > S:
-            break
-        layout.append((b, off, ln))
-        off += pack.padded_length(ln)
-slots = [(ln + 16 + 255) // 256 * 256 for _, _, ln in layout]
-pool = torch.empty(sum(slots) + 4096, dtype=torch.uint8, device=dev)
-pool.random_(0, 256, generator=g)
-starts, pos = [0] * len(layout), 0
-for i in prng.permutation(len(layout)):
-    starts[i] = pos + int(prng.integers(0, 16))
-    pos += slots[i]
-pack_ext = [(pool[starts[i]:], off, ln, b) for i, (b, off, ln) in enumerate(layout)]
-pack_read = sum(ln for _, _, ln in layout)
+lay = TL.layout(B, S, prng)
+pool, starts = TL.distinct_sources(lay, dev, g, prng)
+pack_ext = TL.extents(lay, pool, starts)
+pack_read = sum(ln for _, _, ln in lay)
 torch.cuda.synchronize()
 op("pack_tracts", "pack_kernel", lambda: pack.PackPieces(st[:, 0], S, pack_ext), pack_read + B * S,
    pieces=B, bytes_read=pack_read, bytes_written=B * S)
-verify_ok = bool(oks[-1].all())
-del pool, pack_ext, st, oks
+del pool, pack_ext
+torch.cuda.empty_cache()
+# PackTracts fused with Encode (curator encPack -> encEncode in one pass): every data
+# piece of every stripe packed from distinct tract sources, parity encoded from registers.
+lay = TL.layout(B * k, S, np.random.default_rng(29))
+pool, starts = TL.distinct_sources(lay, dev, g, prng)
+pe_ext = TL.extents(lay, pool, starts)
+pe_read = sum(ln for _, _, ln in lay)
+torch.cuda.synchronize()
+op("pack_encode_rs6_3_distinct", "pack_encode_kernel", lambda: pack.PackEncode(enc, st, pe_ext),
+   pe_read + B * (k + m) * S, pieces=B * k, tracts=len(lay), bytes_read=pe_read, bytes_written=B * (k + m) * S)
+pe_ok = bool(check("verify_after_pack_encode_rs6_3", "rs_code_kernel", lambda: enc.VerifyBatch(st)).all())
+del pool, pe_ext
+torch.cuda.empty_cache()
+verify_ok = bool(oks[-1].all()) and pe_ok
+del st, oks
+torch.cuda.empty_cache()
+
+# blb's COLD class RS(8,3) (storage_class_loop.go:41-44), B=512: PackTracts fused with Encode from
+# distinct tract sources.
+k3, m3, B3 = 8, 3, 512
+st = torch.empty((B3, k3 + m3, S), dtype=torch.uint8, device=dev)
+enc3 = rs.New(k3, m3)
+lay = TL.layout(B3 * k3, S, np.random.default_rng(83))
+pool, starts = TL.distinct_sources(lay, dev, g, prng)
+pe_ext = TL.extents(lay, pool, starts)
+pe_read = sum(ln for _, _, ln in lay)
+torch.cuda.synchronize()
+op("pack_encode_rs8_3_distinct", "pack_encode_kernel", lambda: pack.PackEncode(enc3, st, pe_ext),
+   pe_read + B3 * (k3 + m3) * S, pieces=B3 * k3, tracts=len(lay), bytes_read=pe_read,
+   bytes_written=B3 * (k3 + m3) * S)
+verify_ok = verify_ok and bool(check("verify_after_pack_encode_rs8_3", "rs_code_kernel", lambda: enc3.VerifyBatch(st)).all())
+del pool, pe_ext, st
 torch.cuda.empty_cache()
 
 # blb's widest class: encode and encode fused with the ChecksumFile CRCs on the compiled

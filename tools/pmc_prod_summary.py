@@ -88,6 +88,8 @@ def main():
 
     kernels = {}
     for o in meta["plan"]:
+        if o.get("skip"):  # an untimed check launch between ops
+            continue
         label, algo = o["label"], o["algorithmic_bytes"]
         rd = mean([x[2]["FETCH_SIZE"] for x in f_ops[label]]) * 1024.0 * f_scale
         wr = mean([x[2]["WRITE_SIZE"] for x in w_ops[label]]) * 1024.0 * w_scale
