@@ -130,6 +130,25 @@ class DevPart(ctypes.Structure):
 _lib = None
 
 
+def _one_hip_runtime() -> None:
+    """Make the process's HIP runtime the one torch brings, before libblbrs.so is mapped.
+
+    torch's wheel ships its own libamdhip64 / libhsa-runtime64 (torch/lib, ROCm 7.0) with the
+    same SONAMEs as /opt/rocm's (7.2), which libblbrs.so links.  Loaded after torch, the
+    library's DT_NEEDED entries resolve to torch's copies: one runtime.  Loaded before torch,
+    /opt/rocm's copies are mapped first, torch then maps its own by path, and the process holds
+    two HIP and two HSA runtimes over one /dev/kfd (seen: the second one finds no device).  So
+    import torch first when it is installed; C / C++ / Go callers are not affected (one runtime,
+    /opt/rocm's).  BLBRS_NO_TORCH=1: a ctypes-only process that never imports torch (it then
+    runs on /opt/rocm's runtime alone)."""
+    if os.environ.get("BLBRS_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load() -> ctypes.CDLL:
     """Load libblbrs.so (built by `make -C blb_amd` / __graft_entry__.build())."""
     global _lib
@@ -138,6 +157,7 @@ def load() -> ctypes.CDLL:
             raise ImportError(
                 f"blb_amd: HIP engine library not built ({LIB_PATH} missing); run "
                 "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C blb_amd`")
+        _one_hip_runtime()
         lib = ctypes.CDLL(LIB_PATH)
         # An older build loaded through $BLBRS_LIB_PATH for an A/B run (tools/) may lack the
         # newest entry points; the shipped library must export them all (tests/test_capi.py).

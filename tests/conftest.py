@@ -12,6 +12,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libblbrs.so on the GPU)")
 
 
+@pytest.fixture(autouse=True)
+def _device_idle_after_gpu_test(request):
+    """After every GPU test, wait for the whole device (hipDeviceSynchronize: every stream, the
+    library's workers and lanes included).  A fault raised by work a test issued then fails THAT
+    test (in teardown) instead of surfacing at the next test's first device call."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 @pytest.fixture
 def knob():
     """knob(name, value): set a library tuning knob (blbrs_set_tuning; the library reads the

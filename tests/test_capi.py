@@ -134,3 +134,20 @@ def test_compiled_network_covers_blb_classes(knob):
     assert not rs.New(12, 5).compiled_network()["rtc"]   # the compiled encode network wins
     knob("BLBRS_BITSLICE", 0)
     assert not any(rs.New(12, 5).compiled_network().values())
+
+
+def test_one_hip_runtime_whatever_the_import_order():
+    """torch's wheel carries its own libamdhip64 / libhsa-runtime64 under the SONAMEs libblbrs.so
+    links.  Loading the library before torch used to map /opt/rocm's copies first and torch's
+    second: two HIP runtimes over one /dev/kfd (the second found no device).  _lib.load() now
+    brings torch's runtime in first, so one copy is mapped in either order."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    code = ("import sys; sys.path.insert(0, %r)\nfrom blb_amd import _lib\n_lib.load()\nimport torch\n"
+            "maps = open('/proc/self/maps').read()\n"
+            "print(sorted({l.split()[-1] for l in maps.splitlines() if 'libamdhip64' in l or 'libhsa-runtime64' in l}))"
+            % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, check=True).stdout
+    libs = eval(out.strip().splitlines()[-1])  # a list literal printed above
+    assert sum("libamdhip64" in x for x in libs) == 1 and sum("libhsa-runtime64" in x for x in libs) == 1, libs

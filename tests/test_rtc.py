@@ -154,11 +154,13 @@ def test_gpu_rpc_and_client_shapes_with_networks(k, m, knob):
     miss = bad_sets(k, m)[-1]
     first_k = [j for j in range(k + m) if j not in miss][:k]
     cases.append(([i in first_k for i in range(k + m)], True))
-    for present, data_only in cases:
+    for ci, (present, data_only) in enumerate(cases):
+        print(f"case {ci}: present={[i for i in range(k + m) if present[i]]} data_only={data_only}", flush=True)
         st = torch.from_numpy(host).cuda()
         for i in range(k + m):
             if not present[i]:
                 st[:, i].fill_(0xA5)
+        torch.cuda.synchronize()   # a fault left by earlier work surfaces here, not after the rebuild
         enc.ReconstructBatch(st, present, data_only=data_only)
         got = st.cpu().numpy()
         for i in range(k + m):
@@ -403,7 +405,10 @@ def test_exit_with_a_compile_in_flight(seed):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # A ctypes-only process (no torch): torch's wheel brings its own comgr, whose static
+    # destructors then race a caller-thread compile at exit the same way.
+    env = dict(os.environ, BLBRS_NO_TORCH="1")
     p = subprocess.run([sys.executable, "-c", _EXIT_SCRIPT, root, str(seed)], capture_output=True, text=True,
-                       timeout=120)
+                       timeout=120, env=env)
     assert p.returncode == 0, (p.returncode, p.stdout[-500:], p.stderr[-2000:])
     assert "exiting" in p.stdout

@@ -29,11 +29,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "blb_amd", "libblbrs.so")
 
 
-def _maps_after(code: str) -> str:
-    """/proc/self/maps of a fresh interpreter after `code` ran (library loaded as `lib`)."""
+def _maps_after(code: str, torch_first: bool = False) -> str:
+    """/proc/self/maps of a fresh interpreter after `code` ran (library loaded as `lib`).  Without
+    torch_first the process never imports torch (torch's wheel maps its own hipRTC), so the maps
+    show what the library itself brings in."""
     script = ("import ctypes, sys\nsys.path.insert(0, %r)\nfrom blb_amd import _lib\nlib = _lib.load()\n" % ROOT
               + code + "\nprint(open('/proc/self/maps').read())\n")
-    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ)
+    if not torch_first:
+        env["BLBRS_NO_TORCH"] = "1"
+    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     return p.stdout
 
@@ -184,5 +189,5 @@ run()
 assert rs.rtc_stats()["loaded"] >= 1, rs.rtc_stats()
 print("MAPS2", "libhiprtc" in open("/proc/self/maps").read())
 '''
-    out = _maps_after(code)
-    assert "MAPS1 False" in out and "MAPS2 True" in out, out[-2000:]
+    out = _maps_after(code, torch_first=True)
+    assert "MAPS1" in out and "MAPS2 True" in out, out[-2000:]
