@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 for v in shipped "$@"; do
   if [ $v = shipped ]; then lib=$PWD/blb_amd/libblbrs.so; else lib=$PWD/tools/_build/variants/$v/libblbrs.so; fi
   export BLBRS_LIB_PATH=$lib
+  mkdir -p $out/$v
   timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/$v/fetch -o fetch -- python3 tools/crc_pmc.py > $out/$v/fetch.log 2>&1 \
   && timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $out/$v/trace -o trace -- python3 tools/crc_pmc.py > $out/$v/trace.log 2>&1 \
   || exit 1
