@@ -532,6 +532,51 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         if (ok) *ok = flag ? 0 : 1;
         return BLBRS_OK;
     }
+    // Small staged calls: blb's degraded read of a piece up to 128 KiB + ExtraRoom has its k
+    // replies in plain memory (rpc.GetBuffer does not pool them, pkg/rpc/pool.go:31) and writes
+    // the user's pageable buffer (client/blb/reconstruct.go:172-173).  Staging those by DMA costs
+    // a copy engine round trip per shard, ~100 us per call at 4 KiB.  Instead the
+    // CPU copies the pageable inputs into the worker's pinned bounce buffer, the pointer table
+    // goes there too (tagged, read by the kernel over PCIe: no upload), the kernel reads and
+    // writes the bounce in place, and the CPU copies the outputs back after the one sync.
+    // Store steps only: a verify flag stays on the device path below.
+    size_t bounce_bytes = round_up(batch * n * sizeof(uint64_t), 256);
+    const size_t Sb = round_up(S, 256);
+    for (size_t x = 0; x < batch * n; ++x) bounce_bytes += pageable[x] ? Sb : 0;
+    if (!verify && bounce_bytes <= rt::kBounceMaxBytes) {
+        if ((rc = w->ensure_bounce(bounce_bytes))) return rc;
+        uint8_t* const hb = w->bounce;
+        std::vector<size_t> at(batch * n, 0);
+        size_t pos = round_up(batch * n * sizeof(uint64_t), 256);
+        for (size_t b = 0; b < batch; ++b)
+            for (int i = 0; i < n; ++i) {
+                const size_t x = b * n + i;
+                if (!touched[i] || !pageable[x]) continue;
+                at[x] = pos;
+                view[x] = w->bounce_dev + pos;
+                if (need_in[i]) std::memcpy(hb + pos, shards[x], S);
+                pos += Sb;
+            }
+        Stripes st;
+        st.nshards = n;
+        st.fault = w->fault;
+        st.tag = rt::next_table_tag();
+        if ((rc = rt::tag_entries(view.data(), view.size(), st.tag, reinterpret_cast<uint64_t*>(hb), &st.aligned)))
+            return rc;
+        st.ptrs = reinterpret_cast<const uint64_t*>(w->bounce_dev);
+        for (size_t t = 0; t < steps.size(); ++t)
+            if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
+        const hipError_t e = hipStreamSynchronize(w->s[0]);
+        if (e != hipSuccess) return drain(hip_fail(e, "bounced call"));
+        if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
+        for (size_t b = 0; b < batch; ++b)
+            for (int i = 0; i < n; ++i) {
+                const size_t x = b * n + i;
+                if (touched[i] && pageable[x] && is_out[i]) std::memcpy(shards[x], hb + at[x], S);
+            }
+        if (ok) *ok = 1;
+        return BLBRS_OK;
+    }
     // Staged: units of (stripe, column chunk) alternate over the worker's two streams and two
     // ring slots, so the H2D of unit u+1 overlaps the kernels and D2H of unit u.  A slot is
     // reused two units later on the same stream, i.e. after that unit's D2H -- in stream

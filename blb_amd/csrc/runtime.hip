@@ -412,6 +412,26 @@ int Worker::ensure_stage(size_t bytes) {
     return BLBRS_OK;
 }
 
+int Worker::ensure_bounce(size_t bytes) {
+    if (bytes <= bounce_cap) return BLBRS_OK;
+    if (bounce) (void)hipHostFree(bounce);  // the last call on it ended with a sync of s[0]
+    bounce = nullptr;
+    bounce_dev = 0;
+    bounce_cap = 0;
+    const size_t cap = round_up(std::max<size_t>(bytes, size_t{64} << 10), size_t{64} << 10);
+    BLBRS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&bounce), cap, hipHostMallocDefault));
+    void* d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, bounce, 0);
+    if (e != hipSuccess || !d) {
+        (void)hipHostFree(bounce);
+        bounce = nullptr;
+        return hip_fail(e != hipSuccess ? e : hipErrorInvalidValue, "bounce buffer device mapping");
+    }
+    bounce_dev = reinterpret_cast<uint64_t>(d);
+    bounce_cap = cap;
+    return BLBRS_OK;
+}
+
 int Worker::upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned,
                          uint32_t* tag) {
     if (count > tab_cap) {
@@ -446,8 +466,12 @@ void Worker::destroy() {
     if (tab_host) (void)hipHostFree(tab_host);
     if (tab_dev) (void)hipFree(tab_dev);
     if (fault) (void)hipHostFree(fault);
+    if (bounce) (void)hipHostFree(bounce);
     stage_add(device, -static_cast<int64_t>(stage_cap));
     fault = nullptr;
+    bounce = nullptr;
+    bounce_dev = 0;
+    bounce_cap = 0;
     flag = nullptr;
     stage = nullptr;
     tab_host = nullptr;

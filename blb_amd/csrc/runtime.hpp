@@ -149,6 +149,10 @@ void corrupt_next_table(int slot);
 
 // Staging budget per worker ring slot: k+m shards x chunk bytes fit in it.
 constexpr size_t kStageSlotBudget = size_t{16} << 20;
+// Host calls whose pageable bytes (inputs and outputs, plus the pointer table) fit in this go
+// through the worker's pinned bounce buffer: CPU copies in, the kernel reads and writes it in
+// place over PCIe, CPU copies out -- one launch and one sync instead of a DMA per shard.
+constexpr size_t kBounceMaxBytes = size_t{512} << 10;
 
 struct Worker {
     int device = -1;
@@ -160,7 +164,11 @@ struct Worker {
     uint64_t* tab_dev = nullptr;
     size_t tab_cap = 0;             // entries
     uint32_t* fault = nullptr;      // pinned record of the worker's table checks
+    uint8_t* bounce = nullptr;      // pinned, device-mapped bounce buffer of small staged calls
+    uint64_t bounce_dev = 0;        //   its device address
+    size_t bounce_cap = 0;
     int ensure_stage(size_t bytes);
+    int ensure_bounce(size_t bytes);
     // Copies `count` device addresses, tagged (*tag), to the worker's device table on stream s[0].
     int upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned, uint32_t* tag);
     void destroy();

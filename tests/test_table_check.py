@@ -77,13 +77,17 @@ def _stripe(k, m, S, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pool", [True, False])
-def test_gpu_wrong_tag_host_call_names_slot(pool):
-    """Host Encode (pool buffers: zero copy on the worker's table; pageable: staged, per-chunk
-    tables): an entry with a wrong tag fails the call with ErrHIP naming the slot, the parity is
-    not written, and the next call on the same encoder is bit-exact."""
-    k, m, S = 6, 3, 3 * 16384 + 100
-    truth = _stripe(k, m, S, 11 + pool)
+@pytest.mark.parametrize("kind", ["pool", "bounce", "staged"])
+def test_gpu_wrong_tag_host_call_names_slot(kind):
+    """Host Encode on each host path's table: pool buffers (zero copy, the worker's device table),
+    small pageable shards (the worker's pinned bounce buffer, table read over PCIe) and large
+    pageable shards (device staging by DMA, per-chunk tables).  An entry with a wrong tag fails
+    the call with ErrHIP naming the slot, the parity is not written, and the next call on the
+    same encoder is bit-exact."""
+    k, m = 6, 3
+    S = 3 * 16384 + 100 if kind != "staged" else (1 << 20) + 100   # bounce: <= 512 KiB per call
+    pool = kind == "pool"
+    truth = _stripe(k, m, S, 11 + len(kind))
     enc = rs.New(k, m)
     for slot in (0, k + 1):
         if pool:
@@ -97,7 +101,7 @@ def test_gpu_wrong_tag_host_call_names_slot(pool):
         rs.debug_corrupt_next_table(slot)
         with pytest.raises(rs.ErrHIP, match=f"slot {slot} "):
             enc.Encode(sh)
-        if pool:  # zero copy: the skipped stripe's parity is untouched (staged outputs are unspecified)
+        if kind != "staged":  # in place or bounced: nothing reaches the parity (staged outputs are unspecified)
             for i in range(k, k + m):
                 assert (sh[i] == 0xA5).all(), (slot, i)
         enc.Encode(sh)
