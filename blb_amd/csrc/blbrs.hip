@@ -120,7 +120,10 @@ struct DevPlan {
 };
 
 // Uploads on the current device (== device).
+std::atomic<uint64_t> g_host_plans{0}, g_device_plans{0};  // blbrs_plan_stats
+
 int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
+    g_device_plans.fetch_add(1, std::memory_order_relaxed);
     auto dp = std::make_unique<DevPlan>();
     dp->device = device;
     for (const Pass& ps : hp.passes) {
@@ -189,6 +192,7 @@ struct EncoderCore {
             p->rows.assign(matrix.begin() + static_cast<size_t>(k) * k, matrix.end());
             split_passes(*p);
             slot = p;
+            g_host_plans.fetch_add(1, std::memory_order_relaxed);
         }
         return slot;
     }
@@ -232,6 +236,7 @@ struct EncoderCore {
                 }
         split_passes(*p);
         slot = p;
+        g_host_plans.fetch_add(1, std::memory_order_relaxed);
         return slot;
     }
 
@@ -277,7 +282,10 @@ struct EncoderCore {
         split_passes(*p);
         std::lock_guard<std::mutex> g(mu);
         auto& slot = host_plans[key];
-        if (!slot) slot = p;
+        if (!slot) {
+            slot = p;
+            g_host_plans.fetch_add(1, std::memory_order_relaxed);
+        }
         return slot;
     }
 
@@ -332,19 +340,32 @@ struct blbrs_encoder {
 
 namespace {
 
+// Cores live for the process.  blb's client makes a reedsolomon.New per degraded read and drops
+// it (client/blb/reconstruct.go:166); with cores owned by their handles, every such read freed
+// the core, its device plans with it, and the next read inverted and uploaded its plan again
+// (hipMalloc + hipMemcpy + hipFree per call, ~45 us of a 4 KiB read: profiles/r05/latency).
+// Freeing device plans could also race a kernel still queued on a caller's stream by an
+// asynchronous *_dev call whose encoder had just been dropped.  A process uses a handful of
+// (k, m) classes, and a plan's device memory is a few KB.
 std::mutex g_cores_mu;
-std::map<std::pair<int, int>, std::weak_ptr<EncoderCore>> g_cores;
+std::map<std::pair<int, int>, std::shared_ptr<EncoderCore>>& cores() {
+    static auto* m = new std::map<std::pair<int, int>, std::shared_ptr<EncoderCore>>();  // never destroyed
+    return *m;
+}
 
 // The shared core for (k, m); nullptr when the matrix cannot be built.
 std::shared_ptr<EncoderCore> core_for(int k, int m) {
     std::lock_guard<std::mutex> g(g_cores_mu);
-    auto& w = g_cores[{k, m}];
-    if (auto c = w.lock()) return c;
-    auto c = std::make_shared<EncoderCore>();
-    c->k = k;
-    c->m = m;
-    if (!build_matrix(k, m, c->matrix)) return nullptr;
-    w = c;
+    auto& c = cores()[{k, m}];
+    if (c) return c;
+    auto fresh = std::make_shared<EncoderCore>();
+    fresh->k = k;
+    fresh->m = m;
+    if (!build_matrix(k, m, fresh->matrix)) {
+        cores().erase({k, m});
+        return nullptr;
+    }
+    c = fresh;
     return c;
 }
 
@@ -2010,6 +2031,13 @@ int blbrs_set_worker_limit(int per_device) { return rt::set_worker_limit(per_dev
 int blbrs_get_device_stats(int device, blbrs_device_stats* out) {
     if (!out || device < 0) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
     return rt::device_stats(device, out);
+}
+
+int blbrs_plan_stats(uint64_t* host_plans, uint64_t* device_plans) {
+    if (!host_plans || !device_plans) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    *host_plans = g_host_plans.load();
+    *device_plans = g_device_plans.load();
+    return BLBRS_OK;
 }
 
 int blbrs_trim(void) {

@@ -559,6 +559,14 @@ def trim() -> None:
     _check(_lib.load().blbrs_trim())
 
 
+def plan_stats() -> dict:
+    """Plans built since the process started (blbrs_plan_stats): host (inversions) and device
+    (table uploads)."""
+    h, d = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _check(_lib.load().blbrs_plan_stats(ctypes.byref(h), ctypes.byref(d)))
+    return {"host_plans": h.value, "device_plans": d.value}
+
+
 def set_device(device: int) -> None:
     _check(_lib.load().blbrs_set_device(int(device)))
 

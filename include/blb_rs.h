@@ -277,6 +277,11 @@ int blbrs_set_worker_limit(int per_device);
 int blbrs_get_device_stats(int device, blbrs_device_stats* out);
 /* Frees idle stream workers and idle pooled buffers. */
 int blbrs_trim(void);
+/* Coding plans built since the process started: host plans (matrix inversions, one per (k, m)
+ * and erasure pattern) and device plans (table uploads, one per host plan and device).  Plans
+ * live for the process, so a client's per-read New / ReconstructData / free of the same
+ * pattern (client/blb/reconstruct.go:166-173) builds and uploads once. */
+int blbrs_plan_stats(uint64_t* host_plans, uint64_t* device_plans);
 
 /* ---- pointer-table check ----
  * Every shard-pointer table the library uploads carries a 16-bit tag per upload in bits 48-63

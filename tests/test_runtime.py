@@ -18,6 +18,7 @@ import pytest
 from conftest import ROOT  # noqa: F401
 from blb_amd import _lib
 from blb_amd import reedsolomon as rs
+from oracle import rs_numpy as N
 
 MIB = 1 << 20
 EXTRA = 64 << 10  # disk.ExtraRoom (pkg/disk/checksum_file.go:27)
@@ -292,3 +293,29 @@ def test_batcher_on_device_list():
     finally:
         b.close()
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_gpu_per_read_new_builds_each_plan_once():
+    """blb's client makes reedsolomon.New per degraded read and drops it (client/blb/
+    reconstruct.go:166-173).  Cores live for the process: 50 reads of one erasure pattern through
+    fresh encoders invert and upload its plan once (before round 5 the core died with its last
+    handle, and every read rebuilt and re-uploaded -- hipMalloc + hipMemcpy + hipFree per call)."""
+    import gc
+    k, m, S = 6, 3, 4096
+    rng = np.random.default_rng(66)
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+    full = data + list(N.encode(k, m, data))
+    gc.collect()
+    before = None
+    for i in range(50):
+        enc = rs.New(k, m)
+        sh = [full[j].copy() if j not in (2,) else None for j in range(k)] + [full[j].copy() for j in range(k, k + m)]
+        sh[k + 1] = None   # a parity reply missing too: present = data but 2, parities 6 and 8
+        enc.ReconstructData(sh)
+        assert np.array_equal(sh[2], full[2])
+        del enc
+        gc.collect()
+        if i == 0:
+            before = rs.plan_stats()
+    assert rs.plan_stats() == before, (before, rs.plan_stats())
