@@ -150,12 +150,28 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
         const uint32_t nb = static_cast<uint32_t>(a.S - off < 16 ? a.S - off : 16);
         const bool vec = a.aligned && nb == 16;
         uint32_t acc[MR][4] = {};
-        for (int c = 0; c < a.k; ++c) {
-            uint32_t x[4];
-            const uint8_t* p = shard_ptr<ADDR>(a, b, as_const(a.in_idx)[c]) + off;
-            unpack(vec ? ld16<0>(p) : load_bytes(p, nb), x);
-            madd<MR, 4>(Groups<4>(x), [&](int r) { return as_const(a.tables) + (static_cast<uint32_t>(r) * a.k + c) * 5; },
-                        acc, nr);
+        // Inputs in groups of kSlowBatch, every load of a group issued before its math: a small
+        // host call reads its shards over PCIe (~1-2 us a round trip), and one input at a time
+        // made an RS(12,5) 4 KiB read 12 round trips (25 us of kernel, profiles/r05/latency).
+        constexpr int kSlowBatch = 8;
+        for (int c0 = 0; c0 < a.k; c0 += kSlowBatch) {
+            const int cn = a.k - c0 < kSlowBatch ? a.k - c0 : kSlowBatch;
+            V4 xin[kSlowBatch];
+#pragma unroll
+            for (int j = 0; j < kSlowBatch; ++j) {
+                if (j >= cn) break;
+                const uint8_t* p = shard_ptr<ADDR>(a, b, as_const(a.in_idx)[c0 + j]) + off;
+                xin[j] = vec ? ld16<0>(p) : load_bytes(p, nb);
+            }
+#pragma unroll
+            for (int j = 0; j < kSlowBatch; ++j) {
+                if (j >= cn) break;
+                const int c = c0 + j;
+                uint32_t x[4];
+                unpack(xin[j], x);
+                madd<MR, 4>(Groups<4>(x),
+                            [&](int r) { return as_const(a.tables) + (static_cast<uint32_t>(r) * a.k + c) * 5; }, acc, nr);
+            }
         }
 #pragma unroll
         for (int r = 0; r < MR; ++r) {
