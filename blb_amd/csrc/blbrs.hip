@@ -374,6 +374,8 @@ struct Stripes {
     uint8_t* base = nullptr;  // strided form
     uint64_t shard_stride = 0, stripe_stride = 0;
     const uint64_t* ptrs = nullptr;  // device pointer table form
+    const uint64_t* inl = nullptr;   //   or an inline table (host memory, copied into the launch)
+    uint32_t ninline = 0;            //   of this many entries (<= kInlinePtrs)
     uint32_t nshards = 0;
     bool aligned = false;
     uint32_t tag = 0;                // the table's tag (rt::tag_entries)
@@ -404,6 +406,10 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         a.parity = ps.parity ? 1 : 0;
         a.ptr_tag = st.tag;
         a.fault = st.fault;
+        if (st.ninline) {
+            if (st.ninline > static_cast<uint32_t>(kInlinePtrs)) return fail(BLBRS_ERR_INVALID_ARG, "inline table too long");
+            std::memcpy(a.inl, st.inl, st.ninline * sizeof(uint64_t));
+        }
         Mode m = mode;
         if (mode == Mode::kStoreVerify) {  // per pass: all stored, all compared, or mixed
             a.nstore = ps.nstore;
@@ -538,7 +544,15 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         Stripes st;
         st.nshards = n;
         st.fault = w->fault;
-        if ((rc = w->upload_table(view.data(), view.size(), &st.ptrs, &st.aligned, &st.tag))) return drain(rc);
+        uint64_t inl[kInlinePtrs];
+        if (view.size() <= static_cast<size_t>(kInlinePtrs)) {  // one stripe: the table rides in the launch
+            st.tag = rt::next_table_tag();
+            if ((rc = rt::tag_entries(view.data(), view.size(), st.tag, inl, &st.aligned))) return rc;
+            st.inl = inl;
+            st.ninline = static_cast<uint32_t>(view.size());
+        } else if ((rc = w->upload_table(view.data(), view.size(), &st.ptrs, &st.aligned, &st.tag))) {
+            return drain(rc);
+        }
         hipError_t e = hipSuccess;
         if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
         if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
@@ -557,18 +571,20 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     // replies in plain memory (rpc.GetBuffer does not pool them, pkg/rpc/pool.go:31) and writes
     // the user's pageable buffer (client/blb/reconstruct.go:172-173).  Staging those by DMA costs
     // a copy engine round trip per shard, ~100 us per call at 4 KiB.  Instead the
-    // CPU copies the pageable inputs into the worker's pinned bounce buffer, the pointer table
-    // goes there too (tagged, read by the kernel over PCIe: no upload), the kernel reads and
-    // writes the bounce in place, and the CPU copies the outputs back after the one sync.
+    // CPU copies the pageable inputs into the worker's pinned bounce buffer, the tagged pointer
+    // table rides in the launch arguments (one stripe) or in the bounce (more), the kernel reads
+    // and writes the bounce in place, and the CPU copies the outputs back after the one sync.
     // Store steps only: a verify flag stays on the device path below.
-    size_t bounce_bytes = round_up(batch * n * sizeof(uint64_t), 256);
+    const bool inline_tab = batch * n <= static_cast<size_t>(kInlinePtrs);
+    const size_t tab_bytes = inline_tab ? 0 : round_up(batch * n * sizeof(uint64_t), 256);
+    size_t bounce_bytes = tab_bytes;
     const size_t Sb = round_up(S, 256);
     for (size_t x = 0; x < batch * n; ++x) bounce_bytes += pageable[x] ? Sb : 0;
     if (!verify && bounce_bytes <= rt::kBounceMaxBytes) {
         if ((rc = w->ensure_bounce(bounce_bytes))) return rc;
         uint8_t* const hb = w->bounce;
         std::vector<size_t> at(batch * n, 0);
-        size_t pos = round_up(batch * n * sizeof(uint64_t), 256);
+        size_t pos = tab_bytes;
         for (size_t b = 0; b < batch; ++b)
             for (int i = 0; i < n; ++i) {
                 const size_t x = b * n + i;
@@ -582,9 +598,16 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         st.nshards = n;
         st.fault = w->fault;
         st.tag = rt::next_table_tag();
-        if ((rc = rt::tag_entries(view.data(), view.size(), st.tag, reinterpret_cast<uint64_t*>(hb), &st.aligned)))
+        uint64_t inl[kInlinePtrs];
+        if ((rc = rt::tag_entries(view.data(), view.size(), st.tag, inline_tab ? inl : reinterpret_cast<uint64_t*>(hb),
+                                  &st.aligned)))
             return rc;
-        st.ptrs = reinterpret_cast<const uint64_t*>(w->bounce_dev);
+        if (inline_tab) {
+            st.inl = inl;
+            st.ninline = static_cast<uint32_t>(view.size());
+        } else {
+            st.ptrs = reinterpret_cast<const uint64_t*>(w->bounce_dev);  // read over PCIe (rare: many stripes)
+        }
         for (size_t t = 0; t < steps.size(); ++t)
             if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
         const hipError_t e = hipStreamSynchronize(w->s[0]);

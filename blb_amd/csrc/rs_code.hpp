@@ -53,13 +53,19 @@ namespace code {
 
 using namespace dev;
 
+// Entry idx of stripe b's pointer-table row: the table in memory, or the inline one.
+__device__ __forceinline__ uint64_t table_entry(const CodeArgs& a, uint32_t b, int idx) {
+    const uint64_t pos = static_cast<uint64_t>(b) * a.nshards + idx;
+    return a.ptrs ? as_const(a.ptrs)[pos] : a.inl[pos];
+}
+
 template <int ADDR>
 __device__ __forceinline__ uint8_t* shard_ptr(const CodeArgs& a, uint32_t b, int idx) {
     if constexpr (ADDR == 0)
         return a.base + static_cast<uint64_t>(b) * a.stripe_stride +
                static_cast<uint64_t>(idx) * a.shard_stride;
     else
-        return reinterpret_cast<uint8_t*>(as_const(a.ptrs)[static_cast<uint64_t>(b) * a.nshards + idx] & kPtrMask);
+        return reinterpret_cast<uint8_t*>(table_entry(a, b, idx) & kPtrMask);
 }
 
 // Pointer-table addressing: every entry this pass reads or writes for stripe b must carry the
@@ -72,12 +78,11 @@ __device__ __forceinline__ bool stripe_table_ok(const CodeArgs& a, uint32_t b) {
     if constexpr (ADDR == 0) {
         return true;
     } else {
-        const cu64 row = as_const(a.ptrs) + static_cast<uint64_t>(b) * a.nshards;
         const ci32 in_idx = as_const(a.in_idx), out_idx = as_const(a.out_idx);
         const int n = a.k + a.rows;
         for (int j = 0; j < n; ++j) {
             const int idx = j < a.k ? in_idx[j] : out_idx[j - a.k];
-            const uint64_t e = row[idx];
+            const uint64_t e = table_entry(a, b, idx);
             if (static_cast<uint32_t>(e >> kPtrTagShift) != a.ptr_tag) {
                 if (threadIdx.x == 0) {  // vector stores to the host-mapped record, header last
                     a.fault[1] = b;

@@ -117,11 +117,12 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc:
     const uint64_t tps = (args.S + tile - 1) / tile;
     // Tiles are numbered with 32-bit ints: split huge batches.
     const uint64_t max_b = std::max<uint64_t>(1, 0x7FFFFFFFull / tps);
+    if (!args.base && !args.ptrs && static_cast<uint64_t>(args.B) * args.nshards > kInlinePtrs) return hipErrorInvalidValue;
     for (uint64_t b0 = 0; b0 < args.B; b0 += max_b) {
         CodeArgs a = args;
         a.B = static_cast<uint32_t>(std::min<uint64_t>(max_b, args.B - b0));
         if (a.base) a.base += b0 * a.stripe_stride;
-        else a.ptrs += b0 * a.nshards;
+        else if (a.ptrs) a.ptrs += b0 * a.nshards;  // an inline table never splits (B * nshards <= kInlinePtrs)
         if (a.mismatch) a.mismatch += b0;
         a.tiles_per_stripe = static_cast<uint32_t>(tps);
         const uint64_t total = static_cast<uint64_t>(a.B) * tps;

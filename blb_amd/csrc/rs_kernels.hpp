@@ -10,6 +10,9 @@ namespace blbrs {
 // stripe in the batch.  The same kernel serves Encode (rows = parity rows of M),
 // Reconstruct[Data] (rows = inv(M[valid]) and P*inv(M[valid])) and Verify (rows = parity
 // rows, outputs compared instead of stored).
+// Pointer tables of at most this many entries travel in the kernel arguments (CodeArgs::inl).
+constexpr int kInlinePtrs = 32;
+
 struct CodeArgs {
     const uint32_t* tables;   // device: [rows][k][5] v_perm lookup words (gf256.hpp)
     const int32_t* in_idx;    // device: [k] shard index (within a stripe) of input c
@@ -35,6 +38,11 @@ struct CodeArgs {
     // touched; the kernel records the first entry it finds wrong in *fault (host-mapped).
     uint32_t* fault;          // [8]: valid, stripe, slot, expected tag, entry lo, entry hi
     uint32_t ptr_tag;
+    // Inline table (base == ptrs == null): a host call of one stripe passes its k + m tagged
+    // entries here, so the kernel reads no table from memory.  A table in pinned host memory
+    // cost a dependent PCIe round trip per entry checked (~10 us of a 4 KiB RS(6,3) read), one in
+    // device memory an upload per call.
+    uint64_t inl[kInlinePtrs];
 };
 
 // Table entries: the device address in bits 0-47 (every GPU and host address the runtime hands
