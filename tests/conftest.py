@@ -60,3 +60,23 @@ def golden():
             d = {key: z[key] for key in z.files}
             out[(int(d["k"]), int(d["m"]))] = d
     return out
+
+
+def hip_pointer_info(addr: int) -> dict:
+    """hipPointerGetAttributes(addr) through the process's HIP runtime (torch's): what HIP thinks a
+    host address is (type 0 = unregistered, 1 = host-pinned with its device mapping).  For
+    diagnosing copies of pageable memory that fault."""
+    import ctypes
+    import torch  # noqa: F401  (maps the runtime)
+
+    class Attr(ctypes.Structure):
+        _fields_ = [("type", ctypes.c_int), ("device", ctypes.c_int), ("devicePointer", ctypes.c_void_p),
+                    ("hostPointer", ctypes.c_void_p), ("isManaged", ctypes.c_int), ("allocationFlags", ctypes.c_uint)]
+
+    hip = ctypes.CDLL("libamdhip64.so.7")  # SONAME: resolves to the copy already mapped
+    a = Attr()
+    rc = hip.hipPointerGetAttributes(ctypes.byref(a), ctypes.c_void_p(addr))
+    if rc != 0:
+        hip.hipGetLastError()
+    return {"rc": rc, "type": a.type, "device": a.device, "devicePointer": a.devicePointer,
+            "hostPointer": a.hostPointer, "addr": addr}

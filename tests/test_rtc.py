@@ -18,6 +18,8 @@ import os
 import re
 
 import numpy as np
+
+from conftest import hip_pointer_info
 import pytest
 
 from blb_amd import reedsolomon as rs
@@ -156,6 +158,11 @@ def test_gpu_rpc_and_client_shapes_with_networks(k, m, knob):
     cases.append(([i in first_k for i in range(k + m)], True))
     for ci, (present, data_only) in enumerate(cases):
         print(f"case {ci}: present={[i for i in range(k + m) if present[i]]} data_only={data_only}", flush=True)
+        if ci == 0:   # what HIP thinks of the pageable source before the first copy
+            print("host", host.ctypes.data, host.nbytes, hip_pointer_info(host.ctypes.data),
+                  hip_pointer_info(host.ctypes.data + host.nbytes - 1), rs.pool_stats(),
+                  "lib range", rs.host_numa_node(host.ctypes.data), rs.host_numa_node(host.ctypes.data + host.nbytes - 1),
+                  flush=True)
         st = torch.from_numpy(host).cuda()
         for i in range(k + m):
             if not present[i]:
