@@ -20,8 +20,14 @@ def _device_idle_after_gpu_test(request):
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
+    import time
     import torch
     if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        # A fault the runtime reports asynchronously (after the sync above returned) surfaces in
+        # this test's teardown too: wait a little, then one small copy and a sync of our own.
+        time.sleep(0.05)
+        torch.ones(1024, device="cuda").sum().item()
         torch.cuda.synchronize()
 
 

@@ -32,7 +32,7 @@ for step in "${LIST[@]}"; do
   echo "== $step"
   case "$step" in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+      AMD_LOG_LEVEL=1 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; tail -3 "$OUT/pytest_gpu.log" ;;
     tests:*)
       timeout -k 10 600 python -u -m pytest ${step#tests:} -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu_$n.log" 2>&1
