@@ -1963,12 +1963,9 @@ int blbrs_pack_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_str
     const DevPlan* plan = nullptr;
     if ((rc = enc->dev_plan("E", *hp, dc.dev, &plan))) return rc;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    rt::PtrLease lease;
-    const uint64_t* tdev = nullptr;
-    bool unused = false;
-    if ((rc = lease.upload(table.data(), table.size(), s, &tdev, &unused))) return rc;
-    if (plan->passes.size() == 1) {
-        PackEncodeArgs a{};
+    PackEncodeArgs a{};
+    const bool one_pass = plan->passes.size() == 1;
+    if (one_pass) {
         a.tables = plan->passes[0].tables;
         a.out_idx = plan->passes[0].out_idx;
         a.base = stripes;
@@ -1978,14 +1975,25 @@ int blbrs_pack_encode_dev(blbrs_encoder* enc, uint8_t* stripes, size_t shard_str
         a.B = static_cast<uint32_t>(batch);
         a.k = static_cast<uint32_t>(enc->k);
         a.rows = static_cast<uint32_t>(plan->passes[0].rows);
-        a.table = tdev;
         a.nextents = nextents;
         a.parity = plan->passes[0].parity;
-        if (pack_encode_supported(a)) {
-            const hipError_t e = launch_pack_encode(a, s);
-            if (e != hipSuccess) return hip_fail(e, "launch pack_encode_kernel");
-            return BLBRS_OK;
-        }
+    }
+    const bool fused = one_pass && pack_encode_supported(a);
+    // The extent table and (fused) the pre-pass's layout descriptors share one slot of the
+    // caller-stream ring: reused only after the stream has run this call's launches.
+    rt::PtrLease lease;
+    const uint64_t* tdev = nullptr;
+    bool unused = false;
+    void* scratch = nullptr;
+    if ((rc = lease.upload(table.data(), table.size(), s, &tdev, &unused, nullptr,
+                           fused ? pack_encode_scratch_bytes(a) : 0, &scratch)))
+        return rc;
+    if (fused) {
+        a.table = tdev;
+        a.scratch = scratch;
+        const hipError_t e = launch_pack_encode(a, s);
+        if (e != hipSuccess) return hip_fail(e, "launch pack_encode_kernel");
+        return BLBRS_OK;
     }
     // No fused instantiation: PackTracts into the data shards, then Encode (same bytes).
     hipError_t e = pack_pieces(stripes, shard_stride, npieces, shard_len, tdev, s, static_cast<uint32_t>(enc->k),

@@ -36,7 +36,10 @@ struct PackEncodeArgs {
     const uint64_t* table;    // device extent table (pieces = B * k)
     uint64_t nextents;        // extents in the table
     bool parity = false;      // tables are encode parity rows 0..rows-1 of k (gf_bitslice.hpp)
+    void* scratch = nullptr;  // device: >= pack_encode_scratch_bytes(*this), free for this launch
 };
+// Device scratch the launch needs (the per-(piece, tile) layout descriptors of its pre-pass).
+size_t pack_encode_scratch_bytes(const PackEncodeArgs& a);
 // True when a fused instantiation covers the shape (k in blb's list, rows <= 5, 16-byte
 // aligned base and strides); otherwise the caller packs, then encodes.
 bool pack_encode_supported(const PackEncodeArgs& a);

@@ -43,11 +43,51 @@ struct PEArgs {
     uint8_t* base;
     uint64_t shard_stride, stripe_stride, S;
     uint32_t B, tps, xcd_remap, rows;
-    const uint64_t* table;  // [B*K + 1] first extent of each piece, then [nextents][4] extents
-    uint32_t tile;          // bytes per tile
+    const uint64_t* table;
+    const u32x4* desc;  // [piece][tile]: {sbase lo, sbase hi, first extent, kind}
+    uint32_t tile;      // bytes per tile
 };
 
 enum : uint32_t { kZero = 0, kCopy = 1, kMixed = 2 };
+
+// Pre-pass: one thread per (piece, tile) finds the tile's first extent and its layout, so
+// the main kernel reads one descriptor per piece instead of running K binary searches
+// (dependent scalar loads) before it can issue a single data load.
+__global__ __launch_bounds__(256) void pe_classify_kernel(PEArgs a, uint32_t k, u32x4* desc) {
+    const uint64_t id = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    const uint64_t npieces = static_cast<uint64_t>(a.B) * k;
+    if (id >= npieces * a.tps) return;
+    const uint64_t piece = id / a.tps;
+    const uint64_t t0 = (id - piece * a.tps) * a.tile;
+    const uint64_t t1 = t0 + a.tile < a.S ? t0 + a.tile : a.S;
+    const bool full = t1 - t0 == a.tile;
+    const uint64_t* ex = a.table + npieces + 1;
+    uint64_t lo = a.table[piece];
+    const uint64_t hi = a.table[piece + 1];
+    for (uint64_t n = hi - lo; n > 0;) {
+        const uint64_t half = n >> 1, m = lo + half;
+        if (ex[4 * m + 1] + ex[4 * m + 2] <= t0) {
+            lo = m + 1;
+            n -= half + 1;
+        } else {
+            n = half;
+        }
+    }
+    uint32_t kind = kZero;
+    uint64_t sbase = 0;
+    if (lo != hi) {
+        const uint64_t off = ex[4 * lo + 1], len = ex[4 * lo + 2];
+        if (off < t1) {
+            if (full && off <= t0 && off + len >= t1) {
+                kind = kCopy;
+                sbase = ex[4 * lo] - off;
+            } else {
+                kind = kMixed;
+            }
+        }
+    }
+    desc[id] = u32x4{static_cast<uint32_t>(sbase), static_cast<uint32_t>(sbase >> 32), static_cast<uint32_t>(lo), kind};
+}
 
 // out = bytes [s, s+16) of the 32-byte window lo||hi, s = 4q + r (q, r uniform).
 __device__ __forceinline__ V4 funnel(const V4& a, const V4& b, uint32_t q, uint32_t r) {
@@ -169,39 +209,16 @@ __global__ __launch_bounds__(kPEThreads) void pack_encode_kernel(PEArgs a) {
     uint8_t* stripe = a.base + static_cast<uint64_t>(b) * a.stripe_stride;
     const uint64_t* ex = a.table + static_cast<uint64_t>(a.B) * K + 1;
 
-    // Per piece, the tile's extent layout (uniform over the workgroup): lane p of every wave
-    // finds piece p's first extent ending past the tile start -- K binary searches side by side,
-    // vector loads of the extent table (L2-resident: ~32 B per tract), about two steps for
-    // multi-MiB tracts -- and the values are read back per piece with v_readlane.  (Rounds 2-4
-    // ran the searches in a pre-pass kernel writing a descriptor per (piece, tile): 100-134 MB of
-    // descriptors and 0.7-1.1 ms per launch at blb's shapes, profiles/r05.)
+    // Per piece, the tile's extent layout (uniform, from the pre-pass): lane p of every
+    // wave loads piece p's descriptor -- K loads in parallel -- and the values are read back
+    // per piece with v_readlane.
     uint32_t my_kind = kZero;
     uint64_t my_first = 0, my_sbase = 0;
     if (lane < static_cast<uint32_t>(K)) {
-        const uint64_t piece = static_cast<uint64_t>(b) * K + lane;
-        uint64_t lo = a.table[piece];
-        const uint64_t hi = a.table[piece + 1];
-        for (uint64_t n = hi - lo; n > 0;) {
-            const uint64_t half = n >> 1, mid = lo + half;
-            if (ex[4 * mid + 1] + ex[4 * mid + 2] <= t0) {
-                lo = mid + 1;
-                n -= half + 1;
-            } else {
-                n = half;
-            }
-        }
-        if (lo != hi) {
-            const uint64_t off = ex[4 * lo + 1], len = ex[4 * lo + 2];
-            if (off < t1) {
-                if (full && off <= t0 && off + len >= t1) {
-                    my_kind = kCopy;
-                    my_sbase = ex[4 * lo] - off;
-                } else {
-                    my_kind = kMixed;
-                }
-            }
-        }
-        my_first = lo;
+        const u32x4 d = a.desc[(static_cast<uint64_t>(b) * K + lane) * a.tps + (t0 / kTile)];
+        my_sbase = (static_cast<uint64_t>(d.y) << 32) | d.x;
+        my_first = d.z;
+        my_kind = d.w;
     }
     auto rl64 = [](uint64_t v, int l) -> uint64_t {
         const uint32_t lo32 = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
@@ -361,6 +378,8 @@ hipError_t launch_pack_encode(const PackEncodeArgs& in, hipStream_t stream) {
     if (!pack_encode_supported(in)) return hipErrorInvalidValue;
     const bool cm = bs::use(in.parity, static_cast<int>(in.k), static_cast<int>(in.rows), bs::kWidePack);
     const uint64_t tile = 4096ull * tile_u(in.k, cm);
+    const uint64_t ndesc = static_cast<uint64_t>(in.B) * in.k * ((in.S + tile - 1) / tile);
+    if (ndesc > 0xFFFFFFFFull * 256) return hipErrorInvalidValue;
     PEArgs a{};
     a.tables = in.tables;
     a.out_idx = in.out_idx;
@@ -374,10 +393,30 @@ hipError_t launch_pack_encode(const PackEncodeArgs& in, hipStream_t stream) {
     a.table = in.table;
     a.tile = static_cast<uint32_t>(tile);
     const uint64_t total = static_cast<uint64_t>(in.B) * a.tps;
+    uint64_t grid = total;
     a.xcd_remap = 0;
     if (total >= 64 && total % 8 == 0) a.xcd_remap = 1;
-    hipLaunchKernelGGL(pick(in.k, in.rows, cm), dim3(static_cast<unsigned>(total)), dim3(kPEThreads), 0, stream, a);
-    return hipGetLastError();
+    // Descriptors live in the caller's scratch (the extent table's slot, PtrLease): a per-launch
+    // hipMallocAsync / hipFreeAsync of 100-134 MB cost 0.7-1.1 ms per call at blb's shapes.
+    if (!in.scratch) return hipErrorInvalidValue;
+    u32x4* desc = static_cast<u32x4*>(in.scratch);
+    a.desc = desc;
+    hipError_t e = hipSuccess;
+    hipLaunchKernelGGL(pe_classify_kernel, dim3(static_cast<unsigned>((ndesc + 255) / 256)), dim3(256), 0, stream, a,
+                       in.k, desc);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(pick(in.k, in.rows, cm), dim3(static_cast<unsigned>(grid)),
+                           dim3(kPEThreads), 0, stream, a);
+        e = hipGetLastError();
+    }
+    return e;
+}
+
+size_t pack_encode_scratch_bytes(const PackEncodeArgs& in) {
+    const bool cm = bs::use(in.parity, static_cast<int>(in.k), static_cast<int>(in.rows), bs::kWidePack);
+    const uint64_t tile = 4096ull * tile_u(in.k, cm);
+    return static_cast<size_t>(in.B) * in.k * ((in.S + tile - 1) / tile) * sizeof(u32x4);
 }
 
 }  // namespace blbrs

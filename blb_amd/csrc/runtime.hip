@@ -624,7 +624,8 @@ struct PtrSlot {
     std::mutex mu;
     uint64_t* host = nullptr;
     uint64_t* dev = nullptr;
-    size_t cap = 0;  // entries
+    size_t cap = 0;        // entries of `host`
+    size_t dev_bytes = 0;  // bytes of `dev`: the table, then scratch (PtrLease::upload `extra`)
     hipEvent_t done = nullptr;
 };
 
@@ -656,7 +657,7 @@ PtrLease::~PtrLease() {
 }
 
 int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, const uint64_t** dev_out,
-                     bool* aligned, uint32_t* tag) {
+                     bool* aligned, uint32_t* tag, size_t extra, void** extra_out) {
     int dev = 0;
     BLBRS_HIP_TRY(hipGetDevice(&dev));
     SlotRing& r = ring_of(dev);
@@ -675,21 +676,27 @@ int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, con
             return hip_fail(e, "hipEventSynchronize");
         }
     }
-    if (s.cap < count) {
+    const size_t tab_bytes = round_up(std::max<size_t>(count, 1) * 8, 256);
+    if (s.cap < count || s.dev_bytes < tab_bytes + extra) {
+        // The slot's previous launches are done (the event wait above).
         if (s.host) (void)hipHostFree(s.host);
         if (s.dev) (void)hipFree(s.dev);
         s.host = nullptr;
         s.dev = nullptr;
         s.cap = 0;
+        s.dev_bytes = 0;
         const size_t cap = std::max<size_t>(count, 1024);
+        const size_t dev_bytes = std::max(round_up(cap * 8, 256), tab_bytes + extra);
         hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&s.host), cap * 8, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.dev), cap * 8);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.dev), dev_bytes);
         if (e != hipSuccess) {
             s.mu.unlock();
             return hip_fail(e, "ptr table alloc");
         }
         s.cap = cap;
+        s.dev_bytes = dev_bytes;
     }
+    if (extra_out) *extra_out = extra ? reinterpret_cast<uint8_t*>(s.dev) + tab_bytes : nullptr;
     if (tag) {
         *tag = next_table_tag();
         if (int rc = tag_entries(ptrs, count, *tag, s.host, aligned)) {

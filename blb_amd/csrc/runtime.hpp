@@ -207,8 +207,10 @@ class PtrLease {
     ~PtrLease();
     // Uploads on `stream` (current device); the slot stays busy until the stream has run the
     // kernels that read it.  With `tag`, a shard-pointer table: entries tagged (*tag set).
+    // `extra` > 0: the slot's device buffer also holds `extra` bytes of scratch after the table
+    // (256-byte aligned, *extra_out), free for the launches on `stream` that read the table.
     int upload(const uint64_t* ptrs, size_t count, hipStream_t stream, const uint64_t** dev_out, bool* aligned,
-               uint32_t* tag = nullptr);
+               uint32_t* tag = nullptr, size_t extra = 0, void** extra_out = nullptr);
 
  private:
     PtrSlot* slot_ = nullptr;
