@@ -143,7 +143,7 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
         std::memcpy(host.data() + off_tab, ps.tables.data(), ps.tables.size() * 4);
         HIP_TRY(hipMalloc(&d.mem, bytes));
         dp->passes.push_back(d);  // owned from here on (freed by ~DevPlan)
-        HIP_TRY(hipMemcpy(d.mem, host.data(), bytes, hipMemcpyHostToDevice));
+        HIP_TRY(rt::upload_pinned(d.mem, host.data(), bytes));
         auto* base = static_cast<uint8_t*>(d.mem);
         dp->passes.back().in_idx = reinterpret_cast<const int32_t*>(base);
         dp->passes.back().out_idx = reinterpret_cast<const int32_t*>(base + off_out);
@@ -511,18 +511,12 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         (void)hipStreamSynchronize(w->s[1]);
         return rc_;
     };
-    // Per-slot addressing: device shards are always used in place; pinned host shards are read
-    // and written in place by the kernels (zero copy over PCIe, both link directions busy at
-    // once) and only pageable shards go through the worker's staging ring.  blb's degraded read
-    // has k pool buffers in and the user's pageable Blob.ReadAt buffer out (client/blb/
-    // reconstruct.go:172-173, blob.go:59): one staged slot, not k + 1.  A read-dominated call
-    // under concurrency stages its pinned shards too, by DMA (rt::zero_copy_policy).
-    int nwritten = 0, ntouched = 0;
-    for (int i = 0; i < n; ++i) {
-        nwritten += is_out[i];
-        ntouched += touched[i];
-    }
-    const bool zero_copy = rt::zero_copy_policy(dev, nwritten, ntouched);
+    // Per-slot addressing: device shards and pinned host shards are used in place (pinned ones
+    // read and written by the kernels over PCIe, both link directions busy at once); only
+    // pageable shards are staged.  blb's degraded read has k pool buffers in and the user's
+    // pageable Blob.ReadAt buffer out (client/blb/reconstruct.go:172-173, blob.go:59): one staged
+    // slot, not k + 1.  (Rounds 2-4 also staged pinned inputs of read-dominated calls by DMA when
+    // more than 3 calls were in flight; that path went with the device staging)
     std::vector<uint64_t> view(batch * n, 0);
     std::vector<char> pageable(batch * n, 0);
     int max_staged = 0;  // staged touched slots of the worst stripe
@@ -532,7 +526,7 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             if (!touched[i]) continue;
             int owner = -1;
             const bool visible = rt::device_view(shards[b * n + i], &view[b * n + i], &owner);
-            if (!visible || (!zero_copy && owner < 0)) {
+            if (!visible) {
                 pageable[b * n + i] = 1;
                 ++ns;
             }
@@ -558,29 +552,33 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
         for (size_t t = 0; t < steps.size(); ++t)
             if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
-        int32_t flag = 0;
-        if (verify) e = hipMemcpyAsync(&flag, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
+        if (verify && (rc = w->ensure_bounce(0))) return drain(rc);  // the pinned flag word
+        if (verify) e = hipMemcpyAsync(w->flag_host, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
         const hipError_t f = hipStreamSynchronize(w->s[0]);
         if (e == hipSuccess) e = f;
         if (e != hipSuccess) return drain(hip_fail(e, "zero-copy call"));
         if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
-        if (ok) *ok = flag ? 0 : 1;
+        if (ok) *ok = verify && *w->flag_host ? 0 : 1;
         return BLBRS_OK;
     }
-    // Small staged calls: blb's degraded read of a piece up to 128 KiB + ExtraRoom has its k
+    // Pageable shards are never handed to HIP's copy engines: HIP pins pageable memory on the
+    // fly for such copies, and the GPU suite's intermittent illegal-address fault appeared in
+    // exactly that kind of copy after the tests that register, unregister and stage thousands
+    // of heap buffers.  They go through the worker's pinned, device-mapped staging
+    // instead: the CPU copies inputs in, the kernels read and write the staging in place, the
+    // CPU copies outputs out.
+    //
+    // Small calls (one unit): blb's degraded read of a piece up to 128 KiB + ExtraRoom has its k
     // replies in plain memory (rpc.GetBuffer does not pool them, pkg/rpc/pool.go:31) and writes
-    // the user's pageable buffer (client/blb/reconstruct.go:172-173).  Staging those by DMA costs
-    // a copy engine round trip per shard, ~100 us per call at 4 KiB.  Instead the
-    // CPU copies the pageable inputs into the worker's pinned bounce buffer, the tagged pointer
-    // table rides in the launch arguments (one stripe) or in the bounce (more), the kernel reads
-    // and writes the bounce in place, and the CPU copies the outputs back after the one sync.
-    // Store steps only: a verify flag stays on the device path below.
+    // the user's pageable buffer (client/blb/reconstruct.go:172-173): one launch per step, one
+    // sync, and the tagged pointer table rides in the launch arguments (one stripe) or in the
+    // staging (more).  DMA staging cost ~100 us per 4 KiB read.
     const bool inline_tab = batch * n <= static_cast<size_t>(kInlinePtrs);
     const size_t tab_bytes = inline_tab ? 0 : round_up(batch * n * sizeof(uint64_t), 256);
     size_t bounce_bytes = tab_bytes;
     const size_t Sb = round_up(S, 256);
     for (size_t x = 0; x < batch * n; ++x) bounce_bytes += pageable[x] ? Sb : 0;
-    if (!verify && bounce_bytes <= rt::kBounceMaxBytes) {
+    if (bounce_bytes <= rt::kBounceMaxBytes) {
         if ((rc = w->ensure_bounce(bounce_bytes))) return rc;
         uint8_t* const hb = w->bounce;
         std::vector<size_t> at(batch * n, 0);
@@ -608,108 +606,98 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         } else {
             st.ptrs = reinterpret_cast<const uint64_t*>(w->bounce_dev);  // read over PCIe (rare: many stripes)
         }
+        hipError_t e = hipSuccess;
+        if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
+        if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
         for (size_t t = 0; t < steps.size(); ++t)
             if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
-        const hipError_t e = hipStreamSynchronize(w->s[0]);
-        if (e != hipSuccess) return drain(hip_fail(e, "bounced call"));
+        if (verify) e = hipMemcpyAsync(w->flag_host, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
+        const hipError_t f = hipStreamSynchronize(w->s[0]);
+        if (e == hipSuccess) e = f;
+        if (e != hipSuccess) return drain(hip_fail(e, "staged call"));
         if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
         for (size_t b = 0; b < batch; ++b)
             for (int i = 0; i < n; ++i) {
                 const size_t x = b * n + i;
                 if (touched[i] && pageable[x] && is_out[i]) std::memcpy(shards[x], hb + at[x], S);
             }
-        if (ok) *ok = 1;
+        if (ok) *ok = verify && *w->flag_host ? 0 : 1;
         return BLBRS_OK;
     }
-    // Staged: units of (stripe, column chunk) alternate over the worker's two streams and two
-    // ring slots, so the H2D of unit u+1 overlaps the kernels and D2H of unit u.  A slot is
-    // reused two units later on the same stream, i.e. after that unit's D2H -- in stream
-    // order, no event needed.  A slot holds only the unit's pageable shards; the pointer table
-    // of every unit (staged shards -> their ring place, the rest -> their own memory at the
-    // chunk's column) is built up front and uploaded once.  Device staging is bounded by
-    // 2 x kStageSlotBudget.
-    const size_t Sp = round_up(S, 256);
+    // Larger calls: units of (stripe, column chunk) alternate over two slots of the staging, in
+    // order on s[0].  Before unit u fills its slot, the CPU waits for unit u - 2 (the slot's
+    // previous user, event ev[slot]) and copies that unit's outputs out; so the CPU fills one slot
+    // while the kernels work in the other.  A slot holds the unit's pageable shards (and, past
+    // kInlinePtrs entries, its tagged table); the rest are addressed in place at the chunk's
+    // column.  Staging per worker: 2 x kPinnedSlotBytes.
     size_t chunk = S;
-    if (S > (size_t{2} << 20) || static_cast<size_t>(max_staged) * Sp > rt::kStageSlotBudget)
-        chunk = std::max<size_t>(4096,
-                                 std::min<size_t>(size_t{1} << 20, rt::kStageSlotBudget / max_staged / 256 * 256));
+    const size_t slot_tab = n <= kInlinePtrs ? 0 : round_up(static_cast<size_t>(n) * sizeof(uint64_t), 256);
+    if (slot_tab + static_cast<size_t>(max_staged) * Sb > rt::kPinnedSlotBytes)
+        chunk = std::max<size_t>(4096, (rt::kPinnedSlotBytes - slot_tab) / max_staged / 4096 * 4096);
     const size_t cp = round_up(chunk, 256);
-    const size_t slot_bytes = static_cast<size_t>(max_staged) * cp;
-    if ((rc = w->ensure_stage(2 * slot_bytes))) return rc;
+    const size_t slot_bytes = slot_tab + static_cast<size_t>(max_staged) * cp;
+    if ((rc = w->ensure_bounce(2 * slot_bytes))) return rc;
+    if ((rc = w->ensure_events())) return rc;
     const size_t per_stripe = (S + chunk - 1) / chunk, units = batch * per_stripe;
-    const uint64_t stage_view = reinterpret_cast<uint64_t>(w->stage);
-    std::vector<uint64_t> table(units * n, 0);
-    for (size_t b = 0, u = 0; b < batch; ++b)
-        for (size_t off = 0; off < S; off += chunk, ++u) {
-            const uint64_t slot = stage_view + (u & 1) * slot_bytes;
-            for (int i = 0, r = 0; i < n; ++i) {
-                if (!touched[i]) continue;
-                table[u * n + i] = pageable[b * n + i] ? slot + static_cast<uint64_t>(r++) * cp : view[b * n + i] + off;
-            }
-        }
-    const uint64_t* tab_dev = nullptr;
-    bool tab_aligned = false;
-    uint32_t tab_tag = 0;
-    if ((rc = w->upload_table(table.data(), table.size(), &tab_dev, &tab_aligned, &tab_tag))) return drain(rc);
-    hipEvent_t ev = nullptr;
-    struct EvFree {
-        hipEvent_t& e;
-        ~EvFree() {
-            if (e) (void)hipEventDestroy(e);
-        }
-    } ev_free{ev};
-    {
-        // s[1]'s units read the table (and, verifying, the zeroed flag) queued on s[0].
-        hipError_t e = hipSuccess;
-        if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventRecord(ev, w->s[0]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(w->s[1], ev, 0);
-        if (e != hipSuccess) return drain(hip_fail(e, "staged call setup"));
-    }
-    size_t u = 0;
-    for (size_t b = 0; b < batch; ++b) {
-        uint8_t* const* sh = shards + b * n;
-        for (size_t off = 0; off < S; off += chunk, ++u) {
-            const size_t len = std::min(chunk, S - off);
-            hipStream_t s = w->s[u & 1];
-            uint8_t* slot = w->stage + (u & 1) * slot_bytes;
-            hipError_t e = hipSuccess;
-            for (int i = 0, r = 0; i < n && e == hipSuccess; ++i) {
-                if (!touched[i] || !pageable[b * n + i]) continue;
-                if (need_in[i]) e = hipMemcpyAsync(slot + r * cp, sh[i] + off, len, hipMemcpyHostToDevice, s);
-                ++r;
-            }
-            if (e != hipSuccess) return drain(hip_fail(e, "H2D"));
-            Stripes st;
-            st.ptrs = tab_dev + u * n;
-            st.nshards = n;
-            st.aligned = tab_aligned;
-            st.tag = tab_tag;
-            st.fault = w->fault;
-            for (size_t t = 0; t < steps.size(); ++t)
-                if ((rc = run_plan(*plans[t], st, 1, len, steps[t].mode, w->flag, s))) return drain(rc);
-            for (int i = 0, r = 0; i < n && e == hipSuccess; ++i) {
-                if (!touched[i] || !pageable[b * n + i]) continue;
-                if (is_out[i]) e = hipMemcpyAsync(sh[i] + off, slot + r * cp, len, hipMemcpyDeviceToHost, s);
-                ++r;
-            }
-            if (e != hipSuccess) return drain(hip_fail(e, "D2H"));
-        }
-    }
-    int32_t flag = 0;
     hipError_t e = hipSuccess;
-    if (verify) {
-        e = hipEventRecord(ev, w->s[1]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(w->s[0], ev, 0);
-        if (e == hipSuccess) e = hipMemcpyAsync(&flag, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
+    if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
+    if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
+    // Copies the outputs of unit u (finished) from its slot to the caller's pageable shards.
+    auto copy_out = [&](size_t u) {
+        const size_t b = u / per_stripe, off = (u % per_stripe) * chunk, len = std::min(chunk, S - off);
+        const uint8_t* slot = w->bounce + (u & 1) * slot_bytes + slot_tab;
+        for (int i = 0, r = 0; i < n; ++i) {
+            if (!touched[i] || !pageable[b * n + i]) continue;
+            if (is_out[i]) std::memcpy(shards[b * n + i] + off, slot + static_cast<size_t>(r) * cp, len);
+            ++r;
+        }
+    };
+    for (size_t u = 0; u < units; ++u) {
+        const size_t b = u / per_stripe, off = (u % per_stripe) * chunk, len = std::min(chunk, S - off);
+        const size_t sl = u & 1;
+        if (u >= 2) {
+            if ((e = hipEventSynchronize(w->ev[sl])) != hipSuccess) return drain(hip_fail(e, "staged call"));
+            if ((rc = rt::check_fault(w->fault, "host call"))) return drain(rc);
+            copy_out(u - 2);
+        }
+        uint8_t* const slot = w->bounce + sl * slot_bytes;
+        const uint64_t slot_dev = w->bounce_dev + sl * slot_bytes;
+        uint64_t entries[256];  // n <= 256 (blbrs_new)
+        for (int i = 0, r = 0; i < n; ++i) {
+            entries[i] = 0;
+            if (!touched[i]) continue;
+            if (pageable[b * n + i]) {
+                const size_t at = slot_tab + static_cast<size_t>(r++) * cp;
+                if (need_in[i]) std::memcpy(slot + at, shards[b * n + i] + off, len);
+                entries[i] = slot_dev + at;
+            } else {
+                entries[i] = view[b * n + i] + off;
+            }
+        }
+        Stripes st;
+        st.nshards = n;
+        st.fault = w->fault;
+        st.tag = rt::next_table_tag();
+        uint64_t inl[kInlinePtrs];
+        if ((rc = rt::tag_entries(entries, n, st.tag, slot_tab ? reinterpret_cast<uint64_t*>(slot) : inl, &st.aligned)))
+            return drain(rc);
+        if (slot_tab) {
+            st.ptrs = reinterpret_cast<const uint64_t*>(slot_dev);
+        } else {
+            st.inl = inl;
+            st.ninline = static_cast<uint32_t>(n);
+        }
+        for (size_t t = 0; t < steps.size(); ++t)
+            if ((rc = run_plan(*plans[t], st, 1, len, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
+        if ((e = hipEventRecord(w->ev[sl], w->s[0])) != hipSuccess) return drain(hip_fail(e, "staged call"));
     }
-    const hipError_t f0 = hipStreamSynchronize(w->s[0]);
-    const hipError_t f1 = hipStreamSynchronize(w->s[1]);
-    if (e == hipSuccess) e = f0 != hipSuccess ? f0 : f1;
+    if (verify) e = hipMemcpyAsync(w->flag_host, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
+    const hipError_t f = hipStreamSynchronize(w->s[0]);
+    if (e == hipSuccess) e = f;
     if (e != hipSuccess) return drain(hip_fail(e, "staged call"));
     if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
-    if (ok) *ok = flag ? 0 : 1;
+    for (size_t u = units >= 2 ? units - 2 : 0; u < units; ++u) copy_out(u);
+    if (ok) *ok = verify && *w->flag_host ? 0 : 1;
     return BLBRS_OK;
 }
 
@@ -1795,38 +1783,57 @@ int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out) {
     const hipStream_t s = w->s[0];
     uint32_t* dout = nullptr;  // nblocks entries + one seed word
     HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dout), (nblocks + 1) * 4, s));
+    // The CRCs come back through pinned memory: `out` may be pageable, and pageable memory is
+    // never handed to HIP's copy engines.
+    uint8_t* pout = nullptr;
+    size_t pcap = 0;
+    if ((rc = rt::pool_get(nblocks * 4, &pout, &pcap, /*internal=*/true))) {
+        (void)hipFreeAsync(dout, s);
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
+    struct PoolBack {
+        uint8_t* p;
+        ~PoolBack() { (void)rt::pool_put(p); }
+    } pout_back{pout};
     hipError_t e = hipSuccess;
     if (visible) {
         // Pinned / device memory: in place.
         e = crc32c_blocks(reinterpret_cast<const uint8_t*>(view), len, 1, len, block, 0, nullptr, dout, s);
     } else {
-        // Pageable: chunks of at most one ring slot through the worker's staging (the bound of
-        // blb_rs.h's worker limits, whatever len is).  With block <= the slot a chunk is whole
-        // blocks; a longer block (a whole bulk frame) is continued across chunks: the chunk at
-        // offset `off` starts (off mod block) bytes into block off / block, whose CRC so far is
-        // the seed (crc32.Update) and which the chunk's first entry overwrites.
-        const size_t slot = rt::kStageSlotBudget;
+        // Pageable: chunks of at most one slot through the worker's pinned staging, two slots
+        // alternating: the CPU copies chunk c in while the kernel reads chunk c - 1 in place
+        // (device-mapped pinned memory).  With block <= the slot a chunk is whole blocks; a
+        // longer block (a whole bulk frame) is continued across chunks: the chunk at offset
+        // `off` starts (off mod block) bytes into block off / block, whose CRC so far is the
+        // seed (crc32.Update) and which the chunk's first entry overwrites.
+        const size_t slot = rt::kPinnedSlotBytes;
         const size_t C = block <= slot ? slot / block * block : slot;
-        if ((rc = w->ensure_stage(round_up(std::min(C, len), 256)))) {
+        const size_t cs = round_up(std::min(C, len), 256);
+        if ((rc = w->ensure_bounce(2 * cs)) || (rc = w->ensure_events())) {
             (void)hipFreeAsync(dout, s);
             (void)hipStreamSynchronize(s);
             return rc;
         }
         uint32_t* seed = dout + nblocks;
-        for (size_t off = 0; off < len && e == hipSuccess; off += C) {
+        size_t c = 0;
+        for (size_t off = 0; off < len && e == hipSuccess; off += C, ++c) {
             const size_t clen = std::min(C, len - off), phase = off % block, first = off / block;
-            e = hipMemcpyAsync(w->stage, data + off, clen, hipMemcpyHostToDevice, s);
-            if (e == hipSuccess && phase)
-                e = hipMemcpyAsync(seed, dout + first, 4, hipMemcpyDeviceToDevice, s);
-            if (e == hipSuccess)
-                e = crc32c_blocks(w->stage, clen, 1, clen, block, phase, phase ? seed : nullptr, dout + first, s);
+            const size_t sl = c & 1;
+            if (c >= 2 && (e = hipEventSynchronize(w->ev[sl])) != hipSuccess) break;
+            std::memcpy(w->bounce + sl * cs, data + off, clen);
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(w->bounce_dev + sl * cs);
+            if (phase) e = hipMemcpyAsync(seed, dout + first, 4, hipMemcpyDeviceToDevice, s);
+            if (e == hipSuccess) e = crc32c_blocks(src, clen, 1, clen, block, phase, phase ? seed : nullptr, dout + first, s);
+            if (e == hipSuccess) e = hipEventRecord(w->ev[sl], s);
         }
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, nblocks * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(pout, dout, nblocks * 4, hipMemcpyDeviceToHost, s);
     (void)hipFreeAsync(dout, s);
     const hipError_t f = hipStreamSynchronize(s);
     if (e == hipSuccess) e = f;
     if (e != hipSuccess) return hip_fail(e, "crc32c");
+    std::memcpy(out, pout, nblocks * 4);
     return BLBRS_OK;
 }
 

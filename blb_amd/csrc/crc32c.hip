@@ -28,6 +28,9 @@
 #include <vector>
 
 namespace blbrs {
+namespace rt {
+hipError_t upload_pinned(void* dev, const void* src, size_t n);  // runtime.hpp
+}  // namespace rt
 namespace {
 
 using namespace dev;
@@ -559,7 +562,7 @@ hipError_t crc_consts_for(uint64_t seg, const CrcConsts** out) {
         build_consts(seg, &host);
         CrcConsts* d = nullptr;
         if ((e = hipMalloc(&d, sizeof(CrcConsts))) != hipSuccess) return e;
-        if ((e = hipMemcpy(d, &host, sizeof(CrcConsts), hipMemcpyHostToDevice)) != hipSuccess) {
+        if ((e = rt::upload_pinned(d, &host, sizeof(CrcConsts))) != hipSuccess) {
             (void)hipFree(d);
             return e;
         }

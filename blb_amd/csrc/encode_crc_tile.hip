@@ -41,6 +41,9 @@
 #include "tuning.hpp"
 
 namespace blbrs {
+namespace rt {
+hipError_t upload_pinned(void* dev, const void* src, size_t n);  // runtime.hpp
+}  // namespace rt
 namespace {
 
 using namespace dev;
@@ -731,7 +734,7 @@ hipError_t tile_consts_for(const TileConsts** out) {
         }
         TileConsts* d = nullptr;
         if ((e = hipMalloc(&d, sizeof(TileConsts))) != hipSuccess) return e;
-        if ((e = hipMemcpy(d, &host, sizeof(TileConsts), hipMemcpyHostToDevice)) != hipSuccess) {
+        if ((e = rt::upload_pinned(d, &host, sizeof(TileConsts))) != hipSuccess) {
             (void)hipFree(d);
             return e;
         }

@@ -305,11 +305,6 @@ int lane_stats(int dev, int occ, blbrs_lane_stats* out) {
     return BLBRS_OK;
 }
 
-bool zero_copy_policy(int dev, int written, int touched) {
-    if (const long zc = tune::get(tune::kHostZc); zc >= 0) return zc != 0;  // BLBRS_HOST_ZC (tuning.hpp)
-    return 4 * written >= touched || load_of(dev) <= kZeroCopyMaxCalls;
-}
-
 bool device_view(const void* p, uint64_t* view, int* owner) {
     if (owner) *owner = -1;
     hipPointerAttribute_t attr;
@@ -400,21 +395,17 @@ int check_fault(uint32_t* rec, const char* what) {
 // stream workers
 // ---------------------------------------------------------------------------------------
 
-int Worker::ensure_stage(size_t bytes) {
-    if (bytes <= stage_cap) return BLBRS_OK;
-    if (stage) (void)hipFree(stage);
-    stage_add(device, -static_cast<int64_t>(stage_cap));
-    stage = nullptr;
-    stage_cap = 0;
-    BLBRS_HIP_TRY(hipMalloc(&stage, bytes));
-    stage_cap = bytes;
-    stage_add(device, static_cast<int64_t>(bytes));
+int Worker::ensure_events() {
+    for (auto& e : ev)
+        if (!e) BLBRS_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return BLBRS_OK;
 }
 
 int Worker::ensure_bounce(size_t bytes) {
+    if (!flag_host) BLBRS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&flag_host), 64, hipHostMallocDefault));
     if (bytes <= bounce_cap) return BLBRS_OK;
-    if (bounce) (void)hipHostFree(bounce);  // the last call on it ended with a sync of s[0]
+    if (bounce) (void)hipHostFree(bounce);  // every call that used it ended with a sync of its streams
+    stage_add(device, -static_cast<int64_t>(bounce_cap));
     bounce = nullptr;
     bounce_dev = 0;
     bounce_cap = 0;
@@ -429,6 +420,7 @@ int Worker::ensure_bounce(size_t bytes) {
     }
     bounce_dev = reinterpret_cast<uint64_t>(d);
     bounce_cap = cap;
+    stage_add(device, static_cast<int64_t>(cap));  // reported as the device's staging bytes
     return BLBRS_OK;
 }
 
@@ -462,21 +454,24 @@ void Worker::destroy() {
             x = nullptr;
         }
     if (flag) (void)hipFree(flag);
-    if (stage) (void)hipFree(stage);
     if (tab_host) (void)hipHostFree(tab_host);
     if (tab_dev) (void)hipFree(tab_dev);
     if (fault) (void)hipHostFree(fault);
     if (bounce) (void)hipHostFree(bounce);
-    stage_add(device, -static_cast<int64_t>(stage_cap));
+    if (flag_host) (void)hipHostFree(flag_host);
+    for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
+    stage_add(device, -static_cast<int64_t>(bounce_cap));
     fault = nullptr;
     bounce = nullptr;
+    flag_host = nullptr;
+    ev[0] = ev[1] = nullptr;
     bounce_dev = 0;
     bounce_cap = 0;
     flag = nullptr;
-    stage = nullptr;
     tab_host = nullptr;
     tab_dev = nullptr;
-    stage_cap = tab_cap = 0;
+    tab_cap = 0;
 }
 
 namespace {
@@ -716,6 +711,25 @@ int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, con
     BLBRS_HIP_TRY(hipMemcpyAsync(s.dev, s.host, count * 8, hipMemcpyHostToDevice, stream));
     *dev_out = s.dev;
     return BLBRS_OK;
+}
+
+hipError_t upload_pinned(void* dev, const void* src, size_t n) {
+    if (n == 0) return hipSuccess;
+    static std::mutex mu;
+    static uint8_t* buf = nullptr;  // process lifetime
+    static size_t cap = 0;
+    std::lock_guard<std::mutex> g(mu);
+    if (n > cap) {
+        if (buf) (void)hipHostFree(buf);  // the previous upload was synchronous
+        buf = nullptr;
+        cap = 0;
+        const size_t want = round_up(std::max<size_t>(n, 64 << 10), 64 << 10);
+        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&buf), want, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        cap = want;
+    }
+    std::memcpy(buf, src, n);
+    return hipMemcpy(dev, buf, n, hipMemcpyHostToDevice);
 }
 
 // ---------------------------------------------------------------------------------------

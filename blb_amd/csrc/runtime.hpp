@@ -104,16 +104,6 @@ struct LoadTicket {
     ~LoadTicket();
 };
 
-// Whether a host call codes its pinned host shards in place (zero copy over PCIe) or stages
-// them by DMA like pageable ones (tools/host_paths.py --zc-sweep): zero copy
-// wins at every concurrency when the call writes at least a quarter of the slots it touches
-// (Encode: the kernel's posted writes run beside its reads), and for read-dominated calls
-// (ReconstructData: k in, 1 out) while at most kZeroCopyMaxCalls host calls are in flight on
-// the device (this one included); beyond that the copy engines move the inputs faster.
-// knob BLBRS_HOST_ZC = 1 / 0 (tuning.hpp) forces either way for A/B runs.
-constexpr int64_t kZeroCopyMaxCalls = 3;
-bool zero_copy_policy(int dev, int written, int touched);
-
 // Address under which the GPU reaches `p`: device memory as is, pinned host memory
 // (hipHostMalloc / hipHostRegister) through its device mapping.  False for pageable memory.
 // *owner = the device holding device memory, -1 for host memory.
@@ -147,28 +137,30 @@ void corrupt_next_table(int slot);
 
 // ---- stream workers ----
 
-// Staging budget per worker ring slot: k+m shards x chunk bytes fit in it.
-constexpr size_t kStageSlotBudget = size_t{16} << 20;
 // Host calls whose pageable bytes (inputs and outputs, plus the pointer table) fit in this go
 // through the worker's pinned bounce buffer: CPU copies in, the kernel reads and writes it in
 // place over PCIe, CPU copies out -- one launch and one sync instead of a DMA per shard.
 constexpr size_t kBounceMaxBytes = size_t{512} << 10;
+// Larger calls with pageable shards are cut into units that alternate over two slots of the same
+// pinned staging, each at most this big: the CPU fills one slot while the kernel works in the
+// other.  Pageable memory is never handed to HIP's copy engines.
+constexpr size_t kPinnedSlotBytes = size_t{8} << 20;
 
 struct Worker {
     int device = -1;
     hipStream_t s[2] = {nullptr, nullptr};
     int32_t* flag = nullptr;        // verify mismatch flag (device)
-    uint8_t* stage = nullptr;       // device staging: 2 ring slots
-    size_t stage_cap = 0;
     uint64_t* tab_host = nullptr;   // pinned pointer table
     uint64_t* tab_dev = nullptr;
     size_t tab_cap = 0;             // entries
     uint32_t* fault = nullptr;      // pinned record of the worker's table checks
-    uint8_t* bounce = nullptr;      // pinned, device-mapped bounce buffer of small staged calls
-    uint64_t bounce_dev = 0;        //   its device address
+    uint8_t* bounce = nullptr;      // pinned, device-mapped staging of pageable shards (CPU copies in
+    uint64_t bounce_dev = 0;        //   and out; the kernels read and write it in place)
     size_t bounce_cap = 0;
-    int ensure_stage(size_t bytes);
+    int32_t* flag_host = nullptr;   // pinned landing word of the verify flag
+    hipEvent_t ev[2] = {nullptr, nullptr};  // staging slot reuse (created on first use)
     int ensure_bounce(size_t bytes);
+    int ensure_events();
     // Copies `count` device addresses, tagged (*tag), to the worker's device table on stream s[0].
     int upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned, uint32_t* tag);
     void destroy();
@@ -216,6 +208,10 @@ class PtrLease {
     PtrSlot* slot_ = nullptr;
     hipStream_t stream_ = nullptr;
 };
+
+// Synchronous upload of n bytes of host data through a pinned bounce (pageable memory is never
+// handed to HIP's copy engines).  For small, rare uploads: plans, constant tables.
+hipError_t upload_pinned(void* dev, const void* src, size_t n);
 
 // ---- pinned buffer pool (rpc.GetBuffer / PutBuffer over pinned, device-mapped memory) ----
 // Every pinned byte the pool hands out or registers counts against the live limit; past it

@@ -15,7 +15,6 @@ namespace tune {
 // PackTracts variants, run-time encode networks) are no longer built.
 enum Knob : int {
     kBitslice = 0,   // BLBRS_BITSLICE: compiled encode network 0 = never, 1 = where faster (default), 2 = always
-    kHostZc,         // BLBRS_HOST_ZC: host calls zero copy 1 / by DMA 0 / policy -1 (default)
     kEcPersistent,   // BLBRS_EC_PERSISTENT: fused encode+CRC on the persistent segment kernel, the fallback
                      // for shapes the tile-grid kernel does not take (0; 1 forces it where it applies)
     kRtc,            // BLBRS_RTC: run-time decode networks 0 = off (default), 1 = compiled in the

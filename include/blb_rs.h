@@ -65,7 +65,7 @@ typedef struct {
     uint64_t workers;        /* stream workers alive on the device (<= the worker limit) */
     uint64_t idle;           /* of which idle */
     uint64_t waits;          /* calls that had to wait for a free worker */
-    uint64_t staging_bytes;  /* device staging memory held by the workers */
+    uint64_t staging_bytes;  /* pinned staging memory held by the device's workers */
     uint64_t calls;          /* host-memory calls and host-batch parts run on the device */
     int64_t inflight;        /* of which running now */
 } blbrs_device_stats;
@@ -272,7 +272,8 @@ int blbrs_host_unregister(void* p);
 
 /* ---- runtime limits ---- */
 /* Maximum stream workers per device (default 8, >= 1).  Each holds two streams, a verify
- * flag and at most 2 x 16 MiB of device staging (used for pageable shards only). */
+ * flag and at most 2 x 8 MiB of pinned, device-mapped staging (pageable shards only: the CPU
+ * copies them in and out; pageable memory is never handed to HIP's copy engines). */
 int blbrs_set_worker_limit(int per_device);
 int blbrs_get_device_stats(int device, blbrs_device_stats* out);
 /* Frees idle stream workers and idle pooled buffers. */
@@ -313,9 +314,9 @@ int blbrs_debug_corrupt_next_table(int slot);
 int blbrs_crc32c_dev(const uint8_t* data, size_t stride, size_t batch, size_t len, size_t block,
                      uint32_t* out_dev, void* stream);
 /* Host-memory form: one buffer; out (host) has ceil(len / block) entries.  Pinned / device
- * memory is read in place; pageable memory is staged in chunks of at most 16 MiB (block
- * boundaries kept through the phase / seed continuation below), so a call's device staging
- * stays within the worker bound whatever `len` is. */
+ * memory is read in place; pageable memory is copied by the CPU into pinned staging in chunks
+ * of at most 8 MiB (block boundaries kept through the phase / seed continuation below), so a
+ * call's staging stays within the worker bound whatever `len` is. */
 int blbrs_crc32c(const uint8_t* data, size_t len, size_t block, uint32_t* out);
 
 /* Encode fused with the CRC-32C of the parity it writes, in one pass over HBM: what
@@ -446,7 +447,7 @@ int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t s
 
 /* ---- A/B knobs and run-time networks ---- */
 
-/* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_HOST_ZC, BLBRS_EC_PERSISTENT, BLBRS_RTC,
+/* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_EC_PERSISTENT, BLBRS_RTC,
  * BLBRS_RTC_WIDE; blb_amd/csrc/tuning.hpp), each a choice between shipped policies,
  * start from the environment, read once, and change only here -- never by setenv while the
  * library runs.  INVALID_ARG for an unknown name. */

@@ -48,7 +48,7 @@ def timeit(fn, reps):
 def main():
     dev = torch.device("cuda:0")
     out = {}
-    if "--zc-sweep" in sys.argv:
+    if "--zc-sweep" in sys.argv:  # libraries before round 5 only (BLBRS_HOST_ZC was removed)
         # Zero-copy vs DMA staging of pinned shards (knob BLBRS_HOST_ZC), and the library's
         # default policy (-1), on the pool-buffer calls and the client shape.
         for mode in ("1", "0", "auto"):
