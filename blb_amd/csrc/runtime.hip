@@ -656,8 +656,26 @@ int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, con
     int dev = 0;
     BLBRS_HIP_TRY(hipGetDevice(&dev));
     SlotRing& r = ring_of(dev);
-    PtrSlot& s = r.slots[r.next.fetch_add(1) % SlotRing::kSlots];
-    s.mu.lock();
+    const size_t need = round_up(std::max<size_t>(count, 1) * 8, 256) + extra;
+    PtrSlot* pick = nullptr;
+    if (extra) {
+        // Scratch-carrying uploads (pack_encode's descriptors, ~100 MB at blb's shapes) prefer an
+        // idle slot that is already big enough, so a stream of calls does not reallocate scratch
+        // in every slot of the ring.
+        const unsigned start = r.next.load(std::memory_order_relaxed);
+        for (int j = 0; j < SlotRing::kSlots && !pick; ++j) {
+            PtrSlot& c = r.slots[(start + j) % SlotRing::kSlots];
+            if (c.dev_bytes < need || !c.mu.try_lock()) continue;
+            if (!c.done || hipEventQuery(c.done) == hipSuccess) pick = &c;
+            else c.mu.unlock();
+        }
+        (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+    }
+    if (!pick) {
+        pick = &r.slots[r.next.fetch_add(1) % SlotRing::kSlots];
+        pick->mu.lock();
+    }
+    PtrSlot& s = *pick;
     if (!s.done) {
         const hipError_t e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
         if (e != hipSuccess) {
