@@ -89,7 +89,7 @@ op("crc32c_65532", "crc_stream_kernel", lambda: checksum.ChecksumBatch(st[:, k],
 # no read is served by another tract's cached lines; tools/tract_layout.py).
 prng = np.random.default_rng(17)
 lay = TL.layout(B, S, prng)
-pool, starts = TL.distinct_sources(lay, dev, g, prng)
+pool, starts = TL.distinct_sources(lay, dev, g, prng, jitter=True)  # as rounds 3-4
 pack_ext = TL.extents(lay, pool, starts)
 pack_read = sum(ln for _, _, ln in lay)
 torch.cuda.synchronize()

@@ -7,9 +7,12 @@ is its own source bytes.  Two source sets are built here over the same layout:
 
   shared    every tract is a window of one 4 GiB pool at a random offset (round 2-4's bench):
             windows overlap, so part of the reads can be served by L2 / MALL instead of HBM;
-  distinct  every tract has its own bytes, end to end in a shuffled order (and 0-15 bytes off a
-            256-byte boundary), so every byte read is a distinct HBM byte -- the traffic the
-            algorithmic count assumes.
+  distinct  every tract has its own bytes, each at the start of its own page-aligned buffer (the
+            RPC buffer CtlRead returns, store.go:956-959), in a shuffled order, so every byte
+            read is a distinct HBM byte -- the traffic the algorithmic count assumes.  Within a
+            piece, tract j lands at a multiple of padToLength = 64 KiB - 4, so its source is
+            (-offset) mod 16 in {0, 4, 8, 12} bytes off the piece's 16-byte grid, as in blb.
+            jitter=True adds 0-15 more bytes (rounds 4-5 PMC runs: a harsher, non-blb layout).
 """
 from __future__ import annotations
 
@@ -37,15 +40,16 @@ def layout(npieces: int, S: int, prng, lo: int = 64 << 10, hi: int = 8 << 20) ->
     return out
 
 
-def distinct_sources(lay: list, dev, gen, prng):
+def distinct_sources(lay: list, dev, gen, prng, jitter: bool = False):
     """One device pool holding every tract's own bytes; returns (pool, [start of tract i])."""
     import torch
-    slots = [(ln + 16 + 255) // 256 * 256 for _, _, ln in lay]
+    align = 256 if jitter else 4096
+    slots = [(ln + 16 + align - 1) // align * align for _, _, ln in lay]
     pool = torch.empty(sum(slots) + 4096, dtype=torch.uint8, device=dev)
     pool.random_(0, 256, generator=gen)
     starts, pos = [0] * len(lay), 0
     for i in prng.permutation(len(lay)):
-        starts[i] = pos + int(prng.integers(0, 16))
+        starts[i] = pos + (int(prng.integers(0, 16)) if jitter else 0)
         pos += slots[i]
     return pool, starts
 
