@@ -579,3 +579,49 @@ def test_maximum_shard_counts_vs_oracle(oracle_lib, dev, k, m):
                     assert cur[i] is None, (k, m, i)
                 else:
                     assert np.array_equal(cur[i], ref[i]) and np.array_equal(cur[i], full[i]), (k, m, lost, i)
+
+
+@pytest.mark.parametrize("k,m,S,kind", [
+    (6, 3, 4096, "page"),              # one unit through the pinned bounce, inline table
+    (6, 3, 3 * 1024 * 1024 + 48, "page"),  # 4 units per stripe through the two pinned slots
+    (30, 5, 100_000, "page"),          # n = 35 > kInlinePtrs: the table rides in the slot
+    (30, 5, 100_000, "pin"),           # zero copy with n > kInlinePtrs: the worker's device table
+])
+def test_host_staging_paths_verify_and_reconstruct(oracle_lib, k, m, S, kind):
+    """Every host staging path since round 5 (pageable memory never reaches HIP's copy engines,
+    DESIGN §4h): Encode, Verify and ReconstructAndVerify through the pinned bounce, the chunked
+    two-slot pinning and zero copy, with tables inline, in the slot and on the device.  A parity
+    byte corrupted in the LAST chunk must turn Verify / ReconstructAndVerify false; the rebuilt
+    shards are the oracle's."""
+    rng = np.random.default_rng(S + k)
+    data = rand_shards(rng, k, S)
+    want = oracle_encode(oracle_lib, k, m, data)
+    enc = rs.New(k, m)
+
+    def buf(src):
+        if kind == "pin":
+            b = rs.GetBuffer(S)[:S]
+            b[:] = src
+            return b
+        return src.copy()
+
+    held = []
+    sh = [buf(d) for d in data] + [buf(np.full(S, 0x77, np.uint8)) for _ in range(m)]
+    held += sh
+    enc.Encode(sh)
+    assert all(np.array_equal(sh[k + j], want[j]) for j in range(m)), "encode"
+    assert enc.Verify(sh)
+    sh[k + m - 1][S - 3] ^= 0x40                     # inside the last chunk
+    assert not enc.Verify(sh)
+    sh[k + m - 1][S - 3] ^= 0x40
+    lost = [1, k + 1]
+    cur = [None if i in lost else sh[i] for i in range(k + m)]
+    assert enc.ReconstructAndVerify(cur) is True
+    for i in lost:
+        assert np.array_equal(cur[i], (data + want)[i]), ("rebuilt", i)
+    cur = [None if i in lost else sh[i].copy() for i in range(k + m)]
+    cur[k + m - 1][S - 1] ^= 0x01                    # a present parity piece the decode does not read
+    assert enc.ReconstructAndVerify(cur) is False
+    if kind == "pin":
+        for b in held:
+            rs.PutBuffer(b)
