@@ -146,19 +146,71 @@ __device__ __forceinline__ void flag_mismatch(int32_t* flag, bool bad) {
 
 // Partial / unaligned tiles (runtime k, rows <= MR): 16-byte vector accesses where a
 // chunk is whole and aligned, byte accesses for the shard's ragged end or unaligned shards.
+//
+// A small host call is all partial tile (a 4 KiB shard in a 16 KiB tile) and reads its shards
+// over PCIe, ~1.5 us a round trip: the loads of an input group must all be in flight before
+// the first one is waited for.  Chunks that every lane of the block holds whole and aligned
+// (`all_vec`, uniform) take a branch-free group of kSlowBatch loads (the slots past k re-load
+// input c0, valid and unused) -- with per-lane vector/byte choices the compiler waited for
+// every load in turn (RS(6,3) 4 KiB: 11.9 us of kernel, RS(12,5) 21.7 us, profiles/r05).
+constexpr int kSlowBatch = 8;
+
+template <int MR, int MODE, int ADDR>
+__device__ __forceinline__ void code_chunk_vec(const CodeArgs& a, uint32_t b, uint64_t off) {
+    const int nr = a.rows;
+    const ci32 in_idx = as_const(a.in_idx);
+    uint32_t acc[MR][4] = {};
+    for (int c0 = 0; c0 < a.k; c0 += kSlowBatch) {
+        const int cn = a.k - c0 < kSlowBatch ? a.k - c0 : kSlowBatch;
+        const uint8_t* p[kSlowBatch];
+#pragma unroll
+        for (int j = 0; j < kSlowBatch; ++j) p[j] = shard_ptr<ADDR>(a, b, in_idx[c0 + (j < cn ? j : 0)]) + off;
+        V4 xin[kSlowBatch];
+#pragma unroll
+        for (int j = 0; j < kSlowBatch; ++j) xin[j] = ld16<0>(p[j]);
+#pragma unroll
+        for (int j = 0; j < kSlowBatch; ++j) {
+            if (j >= cn) break;
+            const int c = c0 + j;
+            uint32_t x[4];
+            unpack(xin[j], x);
+            madd<MR, 4>(Groups<4>(x), [&](int r) { return as_const(a.tables) + (static_cast<uint32_t>(r) * a.k + c) * 5; },
+                        acc, nr);
+        }
+    }
+    if constexpr (MODE != 0) {
+        V4 chk[MR];
+#pragma unroll
+        for (int r = 0; r < MR; ++r)
+            if (r < nr && !(MODE == 2 && r < a.nstore)) chk[r] = ld16<0>(shard_ptr<ADDR>(a, b, as_const(a.out_idx)[r]) + off);
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < MR; ++r)
+            if (r < nr && !(MODE == 2 && r < a.nstore)) bad |= neq(chk[r], pack(acc[r]));
+        if (bad) atomicOr(&a.mismatch[b], 1);
+    }
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+        if (r >= nr) break;
+        if (MODE == 0 || (MODE == 2 && r < a.nstore)) st16<0>(shard_ptr<ADDR>(a, b, as_const(a.out_idx)[r]) + off, pack(acc[r]));
+    }
+}
+
 template <int MR, int MODE, int ADDR, int U>
 __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, uint64_t tile_off) {
     const int nr = a.rows;
     for (int u = 0; u < U; ++u) {
-        const uint64_t off = tile_off + (static_cast<uint64_t>(u) * kThreads + threadIdx.x) * kBytesPerThread;
+        const uint64_t chunk0 = tile_off + static_cast<uint64_t>(u) * kThreads * kBytesPerThread;
+        if (chunk0 >= a.S) return;
+        const uint64_t off = chunk0 + static_cast<uint64_t>(threadIdx.x) * kBytesPerThread;
+        if (a.aligned && chunk0 + kThreads * kBytesPerThread <= a.S) {  // uniform over the block
+            code_chunk_vec<MR, MODE, ADDR>(a, b, off);
+            continue;
+        }
         if (off >= a.S) return;
         const uint32_t nb = static_cast<uint32_t>(a.S - off < 16 ? a.S - off : 16);
         const bool vec = a.aligned && nb == 16;
         uint32_t acc[MR][4] = {};
-        // Inputs in groups of kSlowBatch, every load of a group issued before its math: a small
-        // host call reads its shards over PCIe (~1-2 us a round trip), and one input at a time
-        // made an RS(12,5) 4 KiB read 12 round trips (25 us of kernel, profiles/r05/latency).
-        constexpr int kSlowBatch = 8;
         for (int c0 = 0; c0 < a.k; c0 += kSlowBatch) {
             const int cn = a.k - c0 < kSlowBatch ? a.k - c0 : kSlowBatch;
             V4 xin[kSlowBatch];
