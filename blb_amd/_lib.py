@@ -69,6 +69,7 @@ SIGNATURES = {
     "blbrs_get_device_stats": (_I, [_I, _P]),
     "blbrs_trim": (_I, []),
     "blbrs_plan_stats": (_I, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "blbrs_debug_watch_faults": (_I, []),
     "blbrs_table_fault_take": (_I, [_I, _P, ctypes.POINTER(_I)]),
     "blbrs_debug_corrupt_next_table": (_I, [_I]),
     "blbrs_set_device": (_I, [_I]),

@@ -2043,6 +2043,7 @@ int blbrs_host_alloc(size_t n, void** out) {
 
 int blbrs_host_free(void* p) {
     if (!p) return BLBRS_OK;
+    rt::note_released(p, 0, "blbrs_host_free");
     HIP_TRY(hipHostFree(p));
     return BLBRS_OK;
 }
@@ -2058,6 +2059,7 @@ int blbrs_host_register(void* p, size_t n) {
 
 int blbrs_host_unregister(void* p) {
     if (!p) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
+    rt::note_released(p, 0, "blbrs_host_unregister");
     HIP_TRY(hipHostUnregister(p));
     return BLBRS_OK;
 }
@@ -2070,6 +2072,8 @@ int blbrs_get_device_stats(int device, blbrs_device_stats* out) {
     if (!out || device < 0) return fail(BLBRS_ERR_INVALID_ARG, "bad argument");
     return rt::device_stats(device, out);
 }
+
+int blbrs_debug_watch_faults(void) { return rt::watch_faults(); }
 
 int blbrs_plan_stats(uint64_t* host_plans, uint64_t* device_plans) {
     if (!host_plans || !device_plans) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");

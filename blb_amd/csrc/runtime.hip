@@ -3,6 +3,8 @@
 
 #include "tuning.hpp"
 
+#include <dlfcn.h>
+#include <hsa/hsa_ext_amd.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -404,6 +406,7 @@ int Worker::ensure_events() {
 int Worker::ensure_bounce(size_t bytes) {
     if (!flag_host) BLBRS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&flag_host), 64, hipHostMallocDefault));
     if (bytes <= bounce_cap) return BLBRS_OK;
+    note_released(bounce, bounce_cap, "worker staging (grown)");
     if (bounce) (void)hipHostFree(bounce);  // every call that used it ended with a sync of its streams
     stage_add(device, -static_cast<int64_t>(bounce_cap));
     bounce = nullptr;
@@ -429,6 +432,8 @@ int Worker::upload_table(const uint64_t* ptrs, size_t count, const uint64_t** de
     if (count > tab_cap) {
         // The previous copy out of tab_host has completed: every call that used it ended with
         // a sync of s[0].
+        note_released(tab_host, tab_cap * 8, "worker table host (grown)");
+        note_released(tab_dev, tab_cap * 8, "worker table device (grown)");
         if (tab_host) (void)hipHostFree(tab_host);
         if (tab_dev) (void)hipFree(tab_dev);
         tab_host = nullptr;
@@ -453,6 +458,10 @@ void Worker::destroy() {
             (void)hipStreamDestroy(x);
             x = nullptr;
         }
+    note_released(flag, 4, "worker flag (destroy)");
+    note_released(tab_host, tab_cap * 8, "worker table host (destroy)");
+    note_released(tab_dev, tab_cap * 8, "worker table device (destroy)");
+    note_released(bounce, bounce_cap, "worker staging (destroy)");
     if (flag) (void)hipFree(flag);
     if (tab_host) (void)hipHostFree(tab_host);
     if (tab_dev) (void)hipFree(tab_dev);
@@ -731,6 +740,66 @@ int PtrLease::upload(const uint64_t* ptrs, size_t count, hipStream_t stream, con
     return BLBRS_OK;
 }
 
+namespace {
+struct Released {
+    uint64_t lo = 0, hi = 0;
+    const char* what = nullptr;
+    uint64_t seq = 0;
+};
+constexpr size_t kReleasedRing = 4096;
+std::mutex g_rel_mu;
+Released g_rel[kReleasedRing];
+uint64_t g_rel_seq = 0;
+
+hsa_status_t on_system_event(const hsa_amd_event_t* e, void*) {
+    if (!e || e->event_type != HSA_AMD_GPU_MEMORY_FAULT_EVENT) return HSA_STATUS_SUCCESS;
+    const uint64_t a = e->memory_fault.virtual_address;
+    std::fprintf(stderr, "blbrs: GPU memory fault at 0x%llx (reason mask 0x%x)\n", static_cast<unsigned long long>(a),
+                 e->memory_fault.fault_reason_mask);
+    std::unique_lock<std::mutex> g(g_rel_mu, std::try_to_lock);
+    if (g.owns_lock()) {
+        // The fault address is a page (or coarser) address: report ranges within 2 MiB of it.
+        constexpr uint64_t kNear = 2ull << 20;
+        int shown = 0;
+        for (size_t i = 0; i < kReleasedRing && shown < 32; ++i) {
+            const Released& r = g_rel[i];
+            if (!r.what || a + kNear < r.lo || a >= r.hi + kNear) continue;
+            std::fprintf(stderr, "blbrs:   released #%llu (%llu ago) %s [0x%llx, 0x%llx)%s\n",
+                         static_cast<unsigned long long>(r.seq), static_cast<unsigned long long>(g_rel_seq - r.seq),
+                         r.what, static_cast<unsigned long long>(r.lo), static_cast<unsigned long long>(r.hi),
+                         a >= r.lo && a < r.hi ? "  <-- contains the address" : "");
+            ++shown;
+        }
+        std::fprintf(stderr, "blbrs:   %d released range(s) near it of %llu released; live pool/registered node: %d\n", shown,
+                     static_cast<unsigned long long>(g_rel_seq), host_numa_node(reinterpret_cast<const void*>(a)));
+    }
+    return HSA_STATUS_SUCCESS;
+}
+}  // namespace
+
+void note_released(const void* p, size_t n, const char* what) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(g_rel_mu);
+    Released& r = g_rel[g_rel_seq % kReleasedRing];
+    r.lo = reinterpret_cast<uint64_t>(p);
+    r.hi = r.lo + n;
+    r.what = what;
+    r.seq = ++g_rel_seq;
+}
+
+int watch_faults() {
+    static std::once_flag once;
+    static hsa_status_t st = HSA_STATUS_SUCCESS;
+    std::call_once(once, [] {
+        // The HSA runtime HIP itself loaded (never a second copy): looked up, not linked.
+        using Reg = hsa_status_t (*)(hsa_amd_system_event_callback_t, void*);
+        void* h = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_NOLOAD);
+        Reg reg = h ? reinterpret_cast<Reg>(dlsym(h, "hsa_amd_register_system_event_handler")) : nullptr;
+        st = reg ? reg(on_system_event, nullptr) : HSA_STATUS_ERROR;
+    });
+    return st == HSA_STATUS_SUCCESS ? BLBRS_OK : fail(BLBRS_ERR_HIP, "hsa_amd_register_system_event_handler failed");
+}
+
 hipError_t upload_pinned(void* dev, const void* src, size_t n) {
     if (n == 0) return hipSuccess;
     static std::mutex mu;
@@ -861,11 +930,12 @@ int pool_put(uint8_t* b) {
     if (!b) return BLBRS_OK;
     HostPool& p = host_pool();
     bool free_it = false;
+    size_t cap = 0;
     {
         std::lock_guard<std::mutex> g(p.mu);
         auto it = p.live.find(b);
         if (it == p.live.end()) return fail(BLBRS_ERR_INVALID_ARG, "buffer was not allocated by blbrs_buffer_get");
-        const size_t cap = it->second;
+        cap = it->second;
         p.live.erase(it);
         p.live_bytes -= cap;
         ++p.puts;
@@ -880,6 +950,7 @@ int pool_put(uint8_t* b) {
     }
     if (free_it) {
         drop_range(b);
+        note_released(b, cap, "pool buffer (hipHostFree on put)");
         BLBRS_HIP_TRY(hipHostFree(b));
     }
     return BLBRS_OK;
@@ -926,6 +997,7 @@ int pool_unregister(void* ptr) {
         p.registered_bytes -= n;
     }
     drop_range(ptr);
+    note_released(ptr, n, "registered host buffer (hipHostUnregister)");
     BLBRS_HIP_TRY(hipHostUnregister(ptr));
     return BLBRS_OK;
 }
@@ -965,18 +1037,19 @@ int pool_stats(blbrs_pool_stats* out) {
 
 void pool_trim() {
     HostPool& p = host_pool();
-    std::vector<uint8_t*> drop;
+    std::vector<std::pair<uint8_t*, size_t>> drop;
     {
         std::lock_guard<std::mutex> g(p.mu);
-        for (auto& fl : p.free_list) {
-            drop.insert(drop.end(), fl.begin(), fl.end());
-            fl.clear();
+        for (int c = 0; c < kNumClasses; ++c) {
+            for (uint8_t* b : p.free_list[c]) drop.emplace_back(b, kClasses[c]);
+            p.free_list[c].clear();
         }
         p.idle_bytes = 0;
         p.frees += drop.size();
     }
-    for (uint8_t* b : drop) {
+    for (auto [b, cap] : drop) {
         drop_range(b);
+        note_released(b, cap, "pool buffer (hipHostFree on trim)");
         (void)hipHostFree(b);
     }
 }

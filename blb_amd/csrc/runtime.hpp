@@ -209,6 +209,13 @@ class PtrLease {
     hipStream_t stream_ = nullptr;
 };
 
+// ---- GPU memory-fault watch (diagnostics) ----
+// Records a host or device range the library releases (unregistered, freed), kept in a ring of
+// the last few thousand; a GPU memory fault reported by the HSA runtime is printed with the ranges
+// of that ring and of the live pool / registrations that hold the faulting address.
+void note_released(const void* p, size_t n, const char* what);
+int watch_faults();  // registers the HSA system event handler once
+
 // Synchronous upload of n bytes of host data through a pinned bounce (pageable memory is never
 // handed to HIP's copy engines).  For small, rare uploads: plans, constant tables.
 hipError_t upload_pinned(void* dev, const void* src, size_t n);

@@ -284,6 +284,13 @@ int blbrs_trim(void);
  * pattern (client/blb/reconstruct.go:166-173) builds and uploads once. */
 int blbrs_plan_stats(uint64_t* host_plans, uint64_t* device_plans);
 
+/* ---- diagnostics (no blb counterpart) ----
+ * Registers, once per process, an HSA system-event handler that prints a GPU memory fault's
+ * virtual address and reason to stderr, with the host / device ranges the library released
+ * most recently near that address (pool frees and trims, unregistrations, staging and table
+ * growth).  The runtime still ends the process after a fault; this only names the address. */
+int blbrs_debug_watch_faults(void);
+
 /* ---- pointer-table check ----
  * Every shard-pointer table the library uploads carries a 16-bit tag per upload in bits 48-63
  * of each entry, and the coding kernel skips (never dereferences) a stripe holding an entry

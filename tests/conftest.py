@@ -12,11 +12,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libblbrs.so on the GPU)")
 
 
+_WATCHING = False
+
+
 @pytest.fixture(autouse=True)
 def _device_idle_after_gpu_test(request):
     """After every GPU test, wait for the whole device (hipDeviceSynchronize: every stream, the
     library's workers and lanes included).  A fault raised by work a test issued then fails THAT
-    test (in teardown) instead of surfacing at the next test's first device call."""
+    test (in teardown) instead of surfacing at the next test's first device call.  Before the
+    first GPU test it also arms the library's fault watch (blbrs_debug_watch_faults), so a GPU
+    memory fault prints its address and the nearby ranges the library released."""
+    global _WATCHING
+    if not _WATCHING and request.node.get_closest_marker("gpu") is not None:
+        _WATCHING = True
+        from blb_amd import _lib
+        rc = _lib.load().blbrs_debug_watch_faults()
+        import sys
+        print(f"blbrs_debug_watch_faults: {rc}", file=sys.__stderr__, flush=True)
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
