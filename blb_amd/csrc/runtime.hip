@@ -790,14 +790,20 @@ void note_released(const void* p, size_t n, const char* what) {
 int watch_faults() {
     static std::once_flag once;
     static hsa_status_t st = HSA_STATUS_SUCCESS;
+    static std::string why;
     std::call_once(once, [] {
-        // The HSA runtime HIP itself loaded (never a second copy): looked up, not linked.
+        // HIP's initialisation initialises the HSA runtime it loaded (never a second copy, DESIGN
+        // §4h); the handler is looked up in that runtime, not linked.
+        (void)hipFree(nullptr);
         using Reg = hsa_status_t (*)(hsa_amd_system_event_callback_t, void*);
         void* h = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_NOLOAD);
         Reg reg = h ? reinterpret_cast<Reg>(dlsym(h, "hsa_amd_register_system_event_handler")) : nullptr;
         st = reg ? reg(on_system_event, nullptr) : HSA_STATUS_ERROR;
+        if (!h) why = "libhsa-runtime64.so.1 is not loaded";
+        else if (!reg) why = "hsa_amd_register_system_event_handler not found";
+        else if (st != HSA_STATUS_SUCCESS) why = "hsa_amd_register_system_event_handler: status " + std::to_string(st);
     });
-    return st == HSA_STATUS_SUCCESS ? BLBRS_OK : fail(BLBRS_ERR_HIP, "hsa_amd_register_system_event_handler failed");
+    return st == HSA_STATUS_SUCCESS ? BLBRS_OK : fail(BLBRS_ERR_HIP, why);
 }
 
 hipError_t upload_pinned(void* dev, const void* src, size_t n) {

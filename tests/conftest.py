@@ -26,9 +26,12 @@ def _device_idle_after_gpu_test(request):
     if not _WATCHING and request.node.get_closest_marker("gpu") is not None:
         _WATCHING = True
         from blb_amd import _lib
-        rc = _lib.load().blbrs_debug_watch_faults()
-        import sys
-        print(f"blbrs_debug_watch_faults: {rc}", file=sys.__stderr__, flush=True)
+        lib = _lib.load()
+        rc = lib.blbrs_debug_watch_faults()
+        why = "" if rc == 0 else lib.blbrs_last_error().decode()
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", "watch_faults.txt"), "a") as f:
+            f.write(f"blbrs_debug_watch_faults: {rc} {why}\n")
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
