@@ -630,10 +630,22 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     // while the kernels work in the other.  A slot holds the unit's pageable shards (and, past
     // kInlinePtrs entries, its tagged table); the rest are addressed in place at the chunk's
     // column.  Staging per worker: 2 x kPinnedSlotBytes.
+    //
+    // A stripe is split into about kPipelineUnits column chunks of at least kMinUnitBytes, so the
+    // CPU's copies of one chunk overlap the kernels of the next even for a single stripe (blb's
+    // degraded read: one 8 MiB piece copied out while the rest is still decoding).
     size_t chunk = S;
     const size_t slot_tab = n <= kInlinePtrs ? 0 : round_up(static_cast<size_t>(n) * sizeof(uint64_t), 256);
     if (slot_tab + static_cast<size_t>(max_staged) * Sb > rt::kPinnedSlotBytes)
         chunk = std::max<size_t>(4096, (rt::kPinnedSlotBytes - slot_tab) / max_staged / 4096 * 4096);
+    constexpr size_t kPipelineUnits = 8, kMinUnitBytes = size_t{128} << 10;
+    if (batch < kPipelineUnits && chunk > kMinUnitBytes) {
+        const size_t want = batch * ((S + chunk - 1) / chunk) >= kPipelineUnits
+                                ? chunk
+                                : std::max(kMinUnitBytes, round_up((S + kPipelineUnits / batch - 1) / (kPipelineUnits / batch),
+                                                                   size_t{64} << 10));
+        chunk = std::min(chunk, want);
+    }
     const size_t cp = round_up(chunk, 256);
     const size_t slot_bytes = slot_tab + static_cast<size_t>(max_staged) * cp;
     if ((rc = w->ensure_bounce(2 * slot_bytes))) return rc;
@@ -692,11 +704,15 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         if ((e = hipEventRecord(w->ev[sl], w->s[0])) != hipSuccess) return drain(hip_fail(e, "staged call"));
     }
     if (verify) e = hipMemcpyAsync(w->flag_host, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
-    const hipError_t f = hipStreamSynchronize(w->s[0]);
-    if (e == hipSuccess) e = f;
     if (e != hipSuccess) return drain(hip_fail(e, "staged call"));
+    if (units >= 2) {  // the next-to-last unit's copy overlaps the last unit's kernels
+        if ((e = hipEventSynchronize(w->ev[(units - 2) & 1])) != hipSuccess) return drain(hip_fail(e, "staged call"));
+        if ((rc = rt::check_fault(w->fault, "host call"))) return drain(rc);
+        copy_out(units - 2);
+    }
+    if ((e = hipStreamSynchronize(w->s[0])) != hipSuccess) return drain(hip_fail(e, "staged call"));
     if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
-    for (size_t u = units >= 2 ? units - 2 : 0; u < units; ++u) copy_out(u);
+    copy_out(units - 1);
     if (ok) *ok = verify && *w->flag_host ? 0 : 1;
     return BLBRS_OK;
 }
