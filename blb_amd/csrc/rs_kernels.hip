@@ -97,34 +97,6 @@ Choice pick(int k, int rows, Mode mode, bool strided, bool cm = false) {
     return strided ? pick_k<2, 0>(k, rows, false) : pick_k<2, 1>(k, rows, false);
 }
 
-// Narrow launches of host calls (pointer tables): a store pass over fewer tiles than the chip
-// has CUs reads its shards over PCIe, and the read rate then follows how many CUs keep reads in
-// flight, not the bytes each holds (one 128 KiB chunk of a degraded read: 8 blocks at U = 4).
-// U = 1 spreads the same bytes over 4x the blocks.
-constexpr uint64_t kNarrowTiles = 256;
-
-template <int K>
-Choice narrow_rows(int rows) {
-    switch (rows) {
-        case 1: return {rs_code_kernel<K, 1, 0, 1, 1, kNT>, 1, K > 0};
-        case 2: return {rs_code_kernel<K, 2, 0, 1, 1, kNT>, 1, K > 0};
-        case 3: return {rs_code_kernel<K, 3, 0, 1, 1, kNT>, 1, K > 0};
-        case 4: return {rs_code_kernel<K, 4, 0, 1, 1, kNT>, 1, K > 0};
-        case 5: return {rs_code_kernel<K, 5, 0, 1, 1, kNT>, 1, K > 0};
-        default: return {};
-    }
-}
-
-Choice pick_narrow(int k, int rows) {
-    if (rows > kMaxTemplRows) return {};
-    switch (k) {
-#define BLBRS_CASE(KK) case KK: return narrow_rows<KK>(rows);
-        BLBRS_K_LIST(BLBRS_CASE)
-#undef BLBRS_CASE
-        default: return narrow_rows<0>(rows);
-    }
-}
-
 }  // namespace
 
 hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc::NetKernel* net) {
@@ -141,12 +113,6 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc:
         ch.cm = true;
     }
     if (!ch.fn && !rfn) return hipErrorInvalidValue;
-    if (!rfn && !ch.cm && !args.base && mode == Mode::kStore && ch.u > 1 &&
-        static_cast<uint64_t>(args.B) * ((args.S + uint64_t{kTileBytes} * ch.u - 1) / (uint64_t{kTileBytes} * ch.u)) <
-            kNarrowTiles) {
-        const Choice nc = pick_narrow(args.k, args.rows);
-        if (nc.fn) ch = nc;
-    }
     const uint64_t tile = static_cast<uint64_t>(kTileBytes) * ch.u;
     const uint64_t tps = (args.S + tile - 1) / tile;
     // Tiles are numbered with 32-bit ints: split huge batches.
