@@ -631,14 +631,15 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     // kInlinePtrs entries, its tagged table); the rest are addressed in place at the chunk's
     // column.  Staging per worker: 2 x kPinnedSlotBytes.
     //
-    // A stripe is split into about kPipelineUnits column chunks of at least kMinUnitBytes, so the
+    // A stripe is split into about kPipelineUnits column chunks of at least kMinUnitBytes (both
+    // measured: 1 MiB as 4 x 256 KiB, 8 MiB as 8 x 1 MiB), so the
     // CPU's copies of one chunk overlap the kernels of the next even for a single stripe (blb's
     // degraded read: one 8 MiB piece copied out while the rest is still decoding).
     size_t chunk = S;
     const size_t slot_tab = n <= kInlinePtrs ? 0 : round_up(static_cast<size_t>(n) * sizeof(uint64_t), 256);
     if (slot_tab + static_cast<size_t>(max_staged) * Sb > rt::kPinnedSlotBytes)
         chunk = std::max<size_t>(4096, (rt::kPinnedSlotBytes - slot_tab) / max_staged / 4096 * 4096);
-    constexpr size_t kPipelineUnits = 8, kMinUnitBytes = size_t{128} << 10;
+    constexpr size_t kPipelineUnits = 8, kMinUnitBytes = size_t{256} << 10;
     if (batch < kPipelineUnits && chunk > kMinUnitBytes) {
         const size_t want = batch * ((S + chunk - 1) / chunk) >= kPipelineUnits
                                 ? chunk
