@@ -151,3 +151,13 @@ def test_one_hip_runtime_whatever_the_import_order():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, check=True).stdout
     libs = eval(out.strip().splitlines()[-1])  # a list literal printed above
     assert sum("libamdhip64" in x for x in libs) == 1 and sum("libhsa-runtime64" in x for x in libs) == 1, libs
+
+
+@pytest.mark.gpu
+def test_gpu_fault_watch_registers():
+    """blbrs_debug_watch_faults registers its HSA system-event handler in the HSA runtime that HIP
+    loaded: status 0, and again 0 (registered once per process)."""
+    from blb_amd import _lib
+    lib = _lib.load()
+    assert lib.blbrs_debug_watch_faults() == 0, lib.blbrs_last_error()
+    assert lib.blbrs_debug_watch_faults() == 0

@@ -7,7 +7,7 @@ set -o pipefail
 OUT=${1:?out}; VAR=${2:?variant dir}; REPS=${3:-2}
 mkdir -p "$OUT"
 for r in $(seq 1 "$REPS"); do
-  for L in 65536 1048576 8388608; do
+  for L in ${LAT_SIZES:-65536 1048576 8388608}; do
     for v in tree variant; do
       if [ $v = variant ]; then lp="$VAR"; else lp=""; fi
       LD_LIBRARY_PATH="$lp" timeout -k 10 120 tests/cpp/_build/latency_bench $L > "$OUT/one.jsonl" 2>> "$OUT/lat_ab.err" || exit $?
