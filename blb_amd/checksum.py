@@ -10,6 +10,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
+from .hostcopy import to_numpy
 from .reedsolomon import ErrInvalidArgument, _check, _is_torch, _torch_stream
 
 CHECKSUM_BLOCK_DATA = 64 * 1024 - 4  # pkg/disk/checksum_block.go:21-29 blockDataLength
@@ -72,5 +73,6 @@ def _seeds_ptr(seeds, count: int, device):
 
 
 def as_uint32(t) -> np.ndarray:
-    """CRC bits from a torch.int32 tensor as numpy uint32."""
-    return t.cpu().numpy().view(np.uint32)
+    """CRC bits from a torch.int32 tensor as numpy uint32 (copied out through pinned memory,
+    hostcopy.py)."""
+    return to_numpy(t).view(np.uint32)

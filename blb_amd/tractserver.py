@@ -31,6 +31,7 @@ from typing import Optional, Protocol, Sequence
 import numpy as np
 
 from . import pack, reedsolomon, rpc
+from .hostcopy import to_numpy
 from .blbcore import (ENCODE_INCREMENT_PROD, RS_CHUNK_VERSION, TRACT_LENGTH, Error, RSChunkID,
                       TractID, TSAddr)
 
@@ -147,7 +148,7 @@ class Store:
         data, ver = ent
         if ver != version:
             return None, Error.ErrVersionMismatch
-        b = data[off:off + length].cpu().numpy() if off < data.numel() else np.zeros(0, np.uint8)
+        b = to_numpy(data[off:off + length]) if off < data.numel() else np.zeros(0, np.uint8)
         return b, (Error.ErrEOF if len(b) < length else Error.NoError)
 
     # store.go:1014-1040

@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 from blb_amd import pack  # noqa: E402
 from blb_amd import reedsolomon as rs  # noqa: E402
+from blb_amd.hostcopy import to_device, to_numpy
 
 SHAPES = [(k, m) for k in (3, 4, 6, 8, 10, 12) for m in (1, 2, 3, 4, 5)]
 
@@ -38,9 +39,9 @@ def test_network_encode_verify_vs_oracle_and_tables(oracle_lib, k, m, knob):
     knob("BLBRS_BITSLICE", 2)
     enc = rs.New(k, m)
     assert enc.compiled_network()["code"]
-    st = torch.from_numpy(host).cuda()
+    st = to_device(host)
     enc.EncodeBatch(st)
-    got = st.cpu().numpy()
+    got = to_numpy(st)
     for b in range(B):
         want = _oracle_parity(oracle_lib, k, m, [host[b, i] for i in range(k)])
         for j in range(m):
@@ -49,15 +50,15 @@ def test_network_encode_verify_vs_oracle_and_tables(oracle_lib, k, m, knob):
     bad = st.clone()
     bad[1, k + m - 1, 5] ^= 0x40           # inside the first (network) tile
     bad[2, k, S - 3] ^= 0x01               # inside the ragged tail (table path)
-    assert enc.VerifyBatch(bad).cpu().tolist() == [True, False, False]
+    assert to_numpy(enc.VerifyBatch(bad)).tolist() == [True, False, False]
     # the table path writes the same bytes and accepts the network's parity
     knob("BLBRS_BITSLICE", 0)
     assert not enc.compiled_network()["code"]
-    tab = torch.from_numpy(host).cuda()
+    tab = to_device(host)
     enc.EncodeBatch(tab)
     assert torch.equal(tab, st)
     assert bool(enc.VerifyBatch(st).all())
-    assert enc.VerifyBatch(bad).cpu().tolist() == [True, False, False]
+    assert to_numpy(enc.VerifyBatch(bad)).tolist() == [True, False, False]
 
 
 @pytest.mark.parametrize("k,m", [(6, 3), (8, 3), (10, 4), (12, 5), (3, 2), (4, 1), (10, 5)])
@@ -72,9 +73,9 @@ def test_network_encode_crc_vs_oracle(oracle_lib, k, m, knob):
     outs = {}
     for mode in ("2", "0"):
         knob("BLBRS_BITSLICE", int(mode))
-        st = torch.from_numpy(host).cuda()
-        crc = enc.EncodeBatchCRC(st, 65532).cpu().numpy().view(np.uint32)
-        outs[mode] = (st.cpu().numpy(), crc)
+        st = to_device(host)
+        crc = to_numpy(enc.EncodeBatchCRC(st, 65532)).view(np.uint32)
+        outs[mode] = (to_numpy(st), crc)
     assert np.array_equal(outs["2"][0], outs["0"][0]) and np.array_equal(outs["2"][1], outs["0"][1])
     got, crc = outs["2"]
     for b in range(B):

@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 from oracle import rs_numpy as N
+from blb_amd.hostcopy import to_device, to_numpy
 
 CHECK = 0xE3069283  # CRC-32C("123456789"), the standard check value
 
@@ -44,7 +45,7 @@ def test_gpu_crc32c_vs_oracle(oracle_lib, block):
         want = oracle_lib.crc32c_blocks(d, block or n)
         got = checksum.Checksum(d, block)                          # host path (staged)
         assert np.array_equal(got, want), (n, block)
-        t = torch.from_numpy(d).cuda()
+        t = to_device(d)
         got_d = checksum.as_uint32(checksum.Checksum(t, block))    # device path
         assert np.array_equal(got_d, want), (n, block, "dev")
 
@@ -55,7 +56,7 @@ def test_gpu_crc32c_unaligned_and_pinned(oracle_lib):
     torch = _torch()
     rng = np.random.default_rng(3)
     base = rng.integers(0, 256, 300000, dtype=np.uint8)
-    dbase = torch.from_numpy(base).cuda()
+    dbase = to_device(base)
     for off in (1, 2, 3, 5, 16):
         d = base[off:off + 200000]
         want = oracle_lib.crc32c_blocks(d, 65532)
@@ -77,7 +78,7 @@ def test_gpu_crc32c_batch_of_parity_shards(oracle_lib):
     parity = st[:, k:, :].reshape(B * m, S)           # strided rows
     crc_blocks = checksum.as_uint32(checksum.ChecksumBatch(parity, 65532))
     crc_whole = checksum.as_uint32(checksum.ChecksumBatch(parity, 0))
-    host = parity.cpu().numpy()
+    host = to_numpy(parity)
     for r in range(B * m):
         assert np.array_equal(crc_blocks[r], oracle_lib.crc32c_blocks(host[r], 65532)), r
         assert int(crc_whole[r, 0]) == oracle_lib.crc32c(host[r]), r
@@ -100,7 +101,7 @@ def test_gpu_crc32c_aligned_shapes(oracle_lib):
         batch = int(rng.integers(1, 4))
         stride = n + 4 * int(rng.integers(0, 40))
         host = rng.integers(0, 256, (batch, stride), dtype=np.uint8)
-        dev = torch.from_numpy(host).cuda()
+        dev = to_device(host)
         got = checksum.as_uint32(checksum.ChecksumBatch(dev[:, :n], blk))
         for r in range(batch):
             want = oracle_lib.crc32c_blocks(host[r, :n], blk or n)
@@ -137,12 +138,12 @@ def test_gpu_crc32c_at_phase_and_seeds(oracle_lib):
     for block, phase, n in cases:
         for lead in (0, 3):
             B = 3
-            base = torch.from_numpy(rng.integers(0, 256, (B, n + 16), dtype=np.uint8)).cuda()
+            base = to_device(rng.integers(0, 256, (B, n + 16), dtype=np.uint8))
             rows = base[:, lead:lead + n]
             seeds_h = rng.integers(0, 1 << 32, B, dtype=np.uint64).astype(np.uint32)
-            seeds = torch.from_numpy(seeds_h.view(np.int32)).cuda()
+            seeds = to_device(seeds_h.view(np.int32))
             got = checksum.as_uint32(checksum.ChecksumBatch(rows, block, phase=phase, seeds=seeds))
-            host = rows.cpu().numpy()
+            host = to_numpy(rows)
             for b in range(B):
                 want, pos, i = [], 0, 0
                 while pos < n:

@@ -11,6 +11,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from blb_amd import reedsolomon as rs  # noqa: E402
+from blb_amd.hostcopy import to_device, to_numpy
 
 MiB = 1 << 20
 
@@ -20,15 +21,15 @@ def run_case(O, k, m, S, block, B, pad=0, seed=0):
     n = k + m
     host = rng.integers(0, 256, (B, n, S + pad), dtype=np.uint8)
     host[:, k:, :S] = 0xEE                       # un-zeroed output buffers
-    dev_full = torch.from_numpy(host).cuda()
+    dev_full = to_device(host)
     view = dev_full[:, :, :S]                    # strided shards when pad > 0
     enc = rs.New(k, m)
     crc = enc.EncodeBatchCRC(view, block)
-    got = dev_full.cpu().numpy()
+    got = to_numpy(dev_full)
     blk = S if block <= 0 or block > S else block
     nblocks = (S + blk - 1) // blk
     assert tuple(crc.shape) == (m, B, nblocks)
-    crc = crc.cpu().numpy().view(np.uint32)
+    crc = to_numpy(crc).view(np.uint32)
     for b in range(B):
         sh = [host[b, i, :S].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
         O.encode(k, m, sh, use_avx2=True, threads=8)
@@ -154,14 +155,14 @@ def test_encode_crc_piece_in_increment_windows(oracle_lib):
         assert tuple(crc.shape) == (m, B, (phase + ln + blk - 1) // blk)
         last_partial = (off + ln) % blk != 0 and off + ln < L
         for c, acc in ((crc, combined), (crc2, combined2)):
-            h = c.cpu().numpy().view(np.uint32)
+            h = to_numpy(c).view(np.uint32)
             for j in range(m):
                 for b in range(B):
                     acc[j][b].extend(h[j, b, :-1] if last_partial else h[j, b])
         prev = crc[:, :, -1].contiguous()
         prev2 = crc2[:, :, -1]
         off += ln
-    host = piece.cpu().numpy()
+    host = to_numpy(piece)
     for b in range(B):
         sh = [host[b, i] for i in range(k)] + [np.zeros(L, np.uint8) for _ in range(m)]
         O.encode(k, m, sh, use_avx2=True, threads=8)
@@ -189,11 +190,11 @@ def test_encode_crc_phase_and_seed_shapes(oracle_lib, k, m):
         B = 2
         host = rng.integers(0, 256, (B, k + m, S), dtype=np.uint8)
         host[:, k:] = 0x5A
-        dev = torch.from_numpy(host).cuda()
+        dev = to_device(host)
         seeds_h = rng.integers(0, 1 << 32, (m, B), dtype=np.uint64).astype(np.uint32)
-        seeds = torch.from_numpy(seeds_h.view(np.int32)).cuda() if block else None
-        crc = enc.EncodeBatchCRC(dev, block, phase=phase, seeds=seeds).cpu().numpy().view(np.uint32)
-        got = dev.cpu().numpy()
+        seeds = to_device(seeds_h.view(np.int32)) if block else None
+        crc = to_numpy(enc.EncodeBatchCRC(dev, block, phase=phase, seeds=seeds)).view(np.uint32)
+        got = to_numpy(dev)
         blk = block or S
         for b in range(B):
             sh = [host[b, i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
@@ -235,12 +236,12 @@ def test_reconstruct_crc_vs_oracle(oracle_lib, k, m, lost, data_only):
             full[b] = np.stack(sh)
         host = full.copy()
         host[:, list(lost)] = 0xC3
-        dev = torch.from_numpy(host).cuda()
+        dev = to_device(host)
         seeds_h = rng.integers(0, 1 << 32, (len(rows), B), dtype=np.uint64).astype(np.uint32)
-        seeds = torch.from_numpy(seeds_h.view(np.int32)).cuda() if block else None
+        seeds = to_device(seeds_h.view(np.int32)) if block else None
         crc = enc.ReconstructBatchCRC(dev, present, block, data_only=data_only, phase=phase, seeds=seeds)
-        crc = crc.cpu().numpy().view(np.uint32)
-        got = dev.cpu().numpy()
+        crc = to_numpy(crc).view(np.uint32)
+        got = to_numpy(dev)
         blk = block or S
         assert crc.shape[0] == len(rows)
         for b in range(B):

@@ -16,6 +16,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from blb_amd import reedsolomon as rs  # noqa: E402
+from blb_amd.hostcopy import to_device, to_numpy
 
 CASES = 160
 
@@ -49,16 +50,16 @@ def test_random_sweep_vs_oracle(oracle_lib):
         tag = (case, k, m, S, kind, op)
         if kind == "device":
             B = int(rng.integers(1, 4))
-            st = torch.from_numpy(np.stack([np.stack(full)] * B)).to(dev)
+            st = to_device(np.stack([np.stack(full)] * B), dev)
             if op == "encode":
                 st[:, k:] = 0xEE
                 enc.EncodeBatch(st)
-                assert torch.equal(st.cpu(), torch.from_numpy(np.stack([np.stack(full)] * B))), tag
+                assert np.array_equal(to_numpy(st), np.stack([np.stack(full)] * B)), tag
             elif op == "verify":
                 bad = int(rng.integers(0, B))
                 shard, pos = int(rng.integers(0, n)), int(rng.integers(0, S))
                 st[bad, shard, pos] ^= 0x01
-                ok = enc.VerifyBatch(st).cpu().numpy()
+                ok = to_numpy(enc.VerifyBatch(st))
                 assert not ok[bad] and ok.sum() == B - 1, tag
             else:
                 e = int(rng.integers(1, m + 1))

@@ -14,6 +14,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from blb_amd import reedsolomon as rs  # noqa: E402
+from blb_amd.hostcopy import to_device, to_numpy
 
 TRACT = 8 * 1024 * 1024  # core.TractLength (internal/core/constants.go:15)
 
@@ -64,10 +65,10 @@ def test_golden_encode_device_batch(golden, dev):
         host = np.empty((B, k + m, S), np.uint8)
         host[:, :k] = data
         host[:, k:] = 0x5A
-        st = torch.from_numpy(host).to(dev)
+        st = to_device(host, dev)
         enc = rs.New(k, m)
         enc.EncodeBatch(st)
-        got = st.cpu().numpy()
+        got = to_numpy(st)
         for b in range(B):
             assert np.array_equal(got[b, k:], parity), (k, m, i, b)
         assert bool(enc.VerifyBatch(st).all())
@@ -91,7 +92,7 @@ def test_golden_reconstruct_host_and_device(golden, dev):
                         assert (sh[i] is None) == (i in pat)
                 # batched device path, erased shards poisoned first
                 B = 2
-                st = torch.from_numpy(np.stack([np.stack(full)] * B)).to(dev)
+                st = to_device(np.stack([np.stack(full)] * B), dev)
                 want = st.clone()
                 for i in pat:
                     st[:, i] = 0xC3
@@ -180,12 +181,12 @@ def test_random_encode_vs_oracle(oracle_lib, k, m, dev):
         for j in range(m):
             assert np.array_equal(sh[k + j], want[j]), (k, m, S, j)
         # device shards (pointer-table path), one of them deliberately misaligned
-        base = torch.from_numpy(np.stack(data + [np.zeros(S, np.uint8)] * m)).to(dev)
+        base = to_device(np.stack(data + [np.zeros(S, np.uint8)] * m), dev)
         odd = torch.empty(S + 1, dtype=torch.uint8, device=dev)[1:]
         odd.copy_(base[0])
         dsh = [odd] + [base[i] for i in range(1, k + m)]
         enc.Encode(dsh)
-        got = base[k:].cpu().numpy()
+        got = to_numpy(base[k:])
         for j in range(m):
             assert np.array_equal(got[j], want[j]), (k, m, S, j, "dev")
 
@@ -234,11 +235,11 @@ def test_verify_detects_corruption(dev, k, m):
     assert bool(enc.VerifyBatch(st).all())
     st[2, k + 1, S - 1] ^= 1   # last byte (tail path) of a parity shard
     st[4, 0, 12345] ^= 0x80    # a data byte
-    ok = enc.VerifyBatch(st).cpu().tolist()
+    ok = to_numpy(enc.VerifyBatch(st)).tolist()
     assert ok == [True, True, False, True, False]
-    host = [st[2, i].cpu().numpy() for i in range(k + m)]
+    host = [to_numpy(st[2, i]) for i in range(k + m)]
     assert not enc.Verify(host)
-    host0 = [st[0, i].cpu().numpy() for i in range(k + m)]
+    host0 = [to_numpy(st[0, i]) for i in range(k + m)]
     assert enc.Verify(host0)
     assert not enc.Verify([st[2, i] for i in range(k + m)])  # device shards
 
@@ -251,7 +252,7 @@ def test_strided_batch_layouts(oracle_lib, dev):
     big = torch.randint(0, 256, (B, k + m, S + 48), dtype=torch.uint8, device=dev)
     view = big[:, :, 16:16 + S]
     enc.EncodeBatch(view)
-    h = view.cpu().numpy()
+    h = to_numpy(view)
     for b in range(B):
         want = oracle_encode(oracle_lib, k, m, [h[b, i].copy() for i in range(k)])
         for j in range(m):
@@ -330,7 +331,7 @@ def test_large_shard_host_path_chunks(oracle_lib):
 def _sample_check(O, enc, st, k, m, stripes):
     """Oracle check of whole 8 MiB stripes sampled from a device batch."""
     for b in stripes:
-        h = st[b].cpu().numpy()
+        h = to_numpy(st[b])
         want = oracle_encode(O, k, m, [h[i].copy() for i in range(k)])
         for j in range(m):
             assert np.array_equal(h[k + j], want[j]), (b, j)
@@ -400,11 +401,11 @@ def test_cold_class_rs83_b512_full_size(oracle_lib, dev):
     st[:, k:] = 0x5A
     crc = enc.EncodeBatchCRC(st, 65532, phase=256, seeds=seeds)
     assert bool(enc.VerifyBatch(st).all())
-    crc = crc.cpu().numpy().view(np.uint32)
-    sd = seeds.cpu().numpy().view(np.uint32)
+    crc = to_numpy(crc).view(np.uint32)
+    sd = to_numpy(seeds).view(np.uint32)
     first = 65532 - 256
     for b in (0, 511):
-        par = st[b, k:].cpu().numpy()
+        par = to_numpy(st[b, k:])
         for j in range(m):
             want0 = oracle_lib.crc32c(par[j][:first], int(sd[j, b]))
             rest = np.asarray(oracle_lib.crc32c_blocks(par[j][first:], 65532), dtype=np.uint32)
@@ -488,12 +489,12 @@ def test_reconstruct_and_verify_one_pass_vs_oracle(oracle_lib, dev, k, m):
             assert ok == want_ok, (k, m, lost, corrupt)
             for i in lost:
                 assert np.array_equal(cur[i], want[i]), (k, m, lost, corrupt, i)
-            st = torch.from_numpy(np.stack(base + base)).reshape(2, n, S).to(dev)
+            st = to_device((np.stack(base + base)).reshape(2, n, S), dev)
             for i in lost:
                 st[:, i] = 0xA5
-            oks = enc.ReconstructAndVerifyBatch(st, present).cpu().numpy()
+            oks = to_numpy(enc.ReconstructAndVerifyBatch(st, present))
             assert list(oks) == [want_ok, want_ok], (k, m, lost, corrupt)
-            got = st.cpu().numpy()
+            got = to_numpy(st)
             for i in lost:
                 assert np.array_equal(got[0, i], want[i]) and np.array_equal(got[1, i], want[i])
             cases += 1
@@ -540,9 +541,9 @@ def test_constant_data_edge_fixtures(oracle_lib, dev, k, m, fill):
         enc.Encode(sh)
         for j in range(m):
             assert np.array_equal(sh[k + j], want[j]), (k, m, fill, S, j)
-        st = torch.from_numpy(np.stack(data + [np.full(S, 0xA5, np.uint8)] * m)[None]).to(dev)
+        st = to_device(np.stack(data + [np.full(S, 0xA5, np.uint8)] * m)[None], dev)
         enc.EncodeBatch(st)
-        got = st[0, k:].cpu().numpy()
+        got = to_numpy(st[0, k:])
         for j in range(m):
             assert np.array_equal(got[j], want[j]), (k, m, fill, S, j, "dev")
         cur = [None if i in (0, k - 1) else sh[i].copy() for i in range(k + m)]
@@ -564,10 +565,10 @@ def test_maximum_shard_counts_vs_oracle(oracle_lib, dev, k, m):
         sh = [d.copy() for d in data] + [np.full(S, 0x11, np.uint8) for _ in range(m)]
         enc.Encode(sh)
         assert all(np.array_equal(sh[k + j], want[j]) for j in range(m)), (k, m, S)
-        st = torch.from_numpy(np.stack(data + want)[None]).to(dev)
+        st = to_device(np.stack(data + want)[None], dev)
         st[:, k:].fill_(0x5A)
         enc.EncodeBatch(st)
-        assert np.array_equal(st[0].cpu().numpy(), np.stack(data + want)), (k, m, S, "batch")
+        assert np.array_equal(to_numpy(st[0]), np.stack(data + want)), (k, m, S, "batch")
         full = data + want
         lost = sorted(rng.choice(k + m, m, replace=False).tolist())
         for data_only in (False, True):

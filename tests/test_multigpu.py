@@ -16,6 +16,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from blb_amd import multigpu
+from blb_amd.hostcopy import to_device, to_numpy
 
 
 def test_stripe_range_partitions():
@@ -109,7 +110,7 @@ def _engine_worker(rank, world, port, root, out_dir):
         for j in range(k):
             host[i, j] = rng.integers(0, 256, S, dtype=np.uint8)
     host[:, k:] = 0xEE  # stale parity buffers
-    st = torch.from_numpy(host).to(dev)
+    st = to_device(host, dev)
     enc = rs.New(k, m, devices=[local])
     dist.barrier()
     t0 = time.perf_counter()
@@ -124,7 +125,7 @@ def _engine_worker(rank, world, port, root, out_dir):
     torch.cuda.synchronize(dev)
     assert torch.equal(st, encoded), f"rank {rank}: reconstruct differs"
     assert bool(enc.VerifyBatch(st).all())
-    np.save(os.path.join(out_dir, f"engine_rank{rank}.npy"), st[:, k:].cpu().numpy())
+    np.save(os.path.join(out_dir, f"engine_rank{rank}.npy"), to_numpy(st[:, k:]))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -10,6 +10,7 @@ from blb_amd import pack
 from blb_amd.blbcore import (RS_CHUNK_VERSION, Error, RSChunkID, TSAddr, TractID,
                              blob_id_from_parts, tract_id_from_parts)
 from blb_amd.tractserver import MemTractserverTalker, Store
+from blb_amd.hostcopy import to_device, to_numpy
 from oracle import rs_numpy as N
 
 gpu = pytest.mark.gpu
@@ -142,12 +143,12 @@ def test_gpu_pack_pieces_vs_oracle(piece_len):
     rng = np.random.default_rng(piece_len)
     npieces = 3
     pool = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
-    dpool = torch.from_numpy(pool).cuda()
+    dpool = to_device(pool)
     ext = _random_extents(rng, npieces, piece_len, pool.size)
     stride = piece_len + int(rng.integers(0, 33))
     dst = torch.full((npieces, stride), 0xA5, dtype=torch.uint8, device="cuda")  # stale bytes
     pack.PackPieces(dst, piece_len, [(dpool[s:], off, ln, p) for s, off, ln, p in ext])
-    got = dst.cpu().numpy()
+    got = to_numpy(dst)
     for p in range(npieces):
         want = N.pack_piece(piece_len, [(pool[s:s + ln].tobytes(), off) for s, off, ln, q in ext if q == p])
         want = want.ljust(piece_len, b"\0")  # a piece with no extents still spans piece_len
@@ -165,7 +166,7 @@ def test_gpu_pack_kernel_edges_vs_oracle(seed):
     torch = _torch()
     rng = np.random.default_rng(1006 + seed)
     pool = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
-    dpool = torch.from_numpy(pool).cuda()
+    dpool = to_device(pool)
     piece_len = 1_000_003
     ext = _random_extents(rng, 2, piece_len, pool.size)
     p, off = 2, 0
@@ -181,7 +182,7 @@ def test_gpu_pack_kernel_edges_vs_oracle(seed):
     npieces = p + 1
     dst = torch.full((npieces, piece_len), 0xA5, dtype=torch.uint8, device="cuda")
     pack.PackPieces(dst, piece_len, [(dpool[s:], o, ln, q) for s, o, ln, q in ext])
-    got = dst.cpu().numpy()
+    got = to_numpy(dst)
     for q in range(npieces):
         want = N.pack_piece(piece_len, [(pool[s:s + ln].tobytes(), o) for s, o, ln, r in ext if r == q])
         assert got[q].tobytes() == want.ljust(piece_len, b"\0"), q
@@ -198,7 +199,7 @@ def test_gpu_pack_pinned_sources_and_destination():
                 torch.full((2, piece_len), 7, dtype=torch.uint8, device="cuda")):
         pack.PackPieces(dst, piece_len, [(pool[s:], off, ln, p) for s, off, ln, p in ext])
         torch.cuda.synchronize()
-        got = dst.cpu().numpy()
+        got = to_numpy(dst)
         for p in range(2):
             want = N.pack_piece(piece_len, [(pool[s:s + ln].numpy().tobytes(), off)
                                             for s, off, ln, q in ext if q == p]).ljust(piece_len, b"\0")
@@ -234,7 +235,7 @@ def test_gpu_pack_then_encode_matches_oracle():
     for i in range(90):  # ~45 MiB of tracts: enough for k chunks >= 90 % full
         n = int(rng.integers(1, 1 << 20))
         t = _spec(tract_id_from_parts(blob_id_from_parts(1, i + 1), 0), length=n)
-        blobs[id(t)] = torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8)).cuda()
+        blobs[id(t)] = to_device(rng.integers(0, 256, n, dtype=np.uint8))
         tracts.append(t)
     chunks = pack.pack_tracts(tracts, piece_len)[:k]
     assert len(chunks) == k
@@ -244,8 +245,8 @@ def test_gpu_pack_then_encode_matches_oracle():
     pack.PackPieces(stripe[:k], piece_len, ext)
     enc = reedsolomon.New(k, m)
     enc.EncodeBatch(stripe.view(1, k + m, piece_len))
-    got = stripe.cpu().numpy()
-    data = [np.frombuffer(N.pack_piece(piece_len, [(blobs[id(t)].cpu().numpy().tobytes(), t.offset)
+    got = to_numpy(stripe)
+    data = [np.frombuffer(N.pack_piece(piece_len, [(to_numpy(blobs[id(t)]).tobytes(), t.offset)
                                                    for t in c.tracts]).ljust(piece_len, b"\0"), np.uint8)
             for c in chunks]
     for i in range(k):
@@ -285,13 +286,13 @@ def test_gpu_pack_encode_fused_vs_oracle(oracle_lib, k, m, S, layout):
     rng = np.random.default_rng(S + 7 * k + m)
     B = 3
     pool = rng.integers(0, 256, 12 << 20, dtype=np.uint8)
-    dpool = torch.from_numpy(pool).cuda()
+    dpool = to_device(pool)
     mk = _long_extents if layout == "long" else _random_extents
     ext = mk(rng, B * k, S, pool.size)
     st = torch.full((B, k + m, S), 0xEE, dtype=torch.uint8, device="cuda")
     enc = reedsolomon.New(k, m)
     pack.PackEncode(enc, st, [(dpool[s:], off, ln, p) for s, off, ln, p in ext])
-    got = st.cpu().numpy()
+    got = to_numpy(st)
     for b in range(B):
         data = []
         for j in range(k):

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 from oracle import rs_numpy as N
+from blb_amd.hostcopy import to_device, to_numpy
 
 KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "published_kat.json")))
 RS = KAT["reedsolomon"]
@@ -78,9 +79,9 @@ def test_kat_one_encode_gpu():
     B = 70
     host = np.full((B, k + m, 2), 0x33, np.uint8)
     host[:, :k] = np.stack(data)
-    st = torch.from_numpy(host).cuda()
+    st = to_device(host)
     enc.EncodeBatch(st)
-    got = st.cpu().numpy()
+    got = to_numpy(st)
     for b in range(B):
         assert got[b, k:].tolist() == [p.tolist() for p in parity], b
     # every 5-of-10 erasure pattern that loses data recovers TestOneEncode's data

@@ -22,6 +22,7 @@ from conftest import ROOT  # noqa: F401
 from blb_amd import _lib, rpc
 from blb_amd import reedsolomon as rs
 from blb_amd.blbcore import Error
+from blb_amd.hostcopy import to_numpy, from_numpy_pinned
 
 MIB = 1 << 20
 
@@ -119,13 +120,13 @@ class _Slots:
         import torch
         b = self.bufs[i]
         if self.kinds[i] == "dev":
-            b.copy_(torch.from_numpy(host))
+            b.copy_(from_numpy_pinned(host))
         else:
             b[:] = host
 
     def get(self, i):
         b = self.bufs[i]
-        return b.cpu().numpy() if self.kinds[i] == "dev" else b.copy()
+        return to_numpy(b) if self.kinds[i] == "dev" else b.copy()
 
     def poison(self, i):
         import torch

@@ -19,10 +19,10 @@ import re
 
 import numpy as np
 
-from conftest import hip_pointer_info
 import pytest
 
 from blb_amd import reedsolomon as rs
+from blb_amd.hostcopy import from_numpy_pinned, to_device, to_numpy
 from oracle import rs_numpy as N
 
 CLASSES = [(6, 3), (8, 3), (10, 3), (12, 5)]  # internal/core/StorageClass.go:7-13
@@ -158,18 +158,13 @@ def test_gpu_rpc_and_client_shapes_with_networks(k, m, knob):
     cases.append(([i in first_k for i in range(k + m)], True))
     for ci, (present, data_only) in enumerate(cases):
         print(f"case {ci}: present={[i for i in range(k + m) if present[i]]} data_only={data_only}", flush=True)
-        if ci == 0:   # what HIP thinks of the pageable source before the first copy
-            print("host", host.ctypes.data, host.nbytes, hip_pointer_info(host.ctypes.data),
-                  hip_pointer_info(host.ctypes.data + host.nbytes - 1), rs.pool_stats(),
-                  "lib range", rs.host_numa_node(host.ctypes.data), rs.host_numa_node(host.ctypes.data + host.nbytes - 1),
-                  flush=True)
-        st = torch.from_numpy(host).cuda()
+        st = to_device(host)
         for i in range(k + m):
             if not present[i]:
                 st[:, i].fill_(0xA5)
         torch.cuda.synchronize()   # a fault left by earlier work surfaces here, not after the rebuild
         enc.ReconstructBatch(st, present, data_only=data_only)
-        got = st.cpu().numpy()
+        got = to_numpy(st)
         for i in range(k + m):
             if present[i] or (data_only and i >= k):
                 continue
@@ -205,12 +200,12 @@ def test_gpu_network_verify_modes_flag_corruption(k, m, knob):
     present = [i not in miss for i in range(k + m)]
     bad = host.copy()
     bad[1, k + m - 1, 5000] ^= 0x40        # a leftover parity piece of stripe 1, inside tile 0
-    st = torch.from_numpy(bad).cuda()
+    st = to_device(bad)
     for i in miss:
         st[:, i].fill_(0xA5)
-    ok = enc.ReconstructAndVerifyBatch(st, present).cpu().numpy()
+    ok = to_numpy(enc.ReconstructAndVerifyBatch(st, present))
     assert list(ok) == [True, False, True], ok
-    got = st.cpu().numpy()
+    got = to_numpy(st)
     for i in miss:
         assert np.array_equal(got[:, i], host[:, i]), i
     for b, want in ((0, True), (1, False)):
@@ -239,7 +234,7 @@ def test_gpu_network_verify_k_outside_compiled_list(knob):
     bad = host.copy()
     bad[0, k + 2, 100] ^= 1                # parity
     bad[2, 7, 20000] ^= 0x80               # data
-    ok = enc.VerifyBatch(torch.from_numpy(bad).cuda()).cpu().numpy()
+    ok = to_numpy(enc.VerifyBatch(to_device(bad)))
     assert list(ok) == [False, True, False], ok
     assert rs.rtc_stats()["loaded"] > before["loaded"]
     assert rs.rtc_stats()["failed"] == before["failed"]
@@ -258,12 +253,12 @@ def test_gpu_network_async_then_loaded(knob):
     enc = rs.New(k, m)
     present = rpc_present(k, m, [2, 9])
     for _ in range(2):
-        st = torch.from_numpy(host).cuda()
+        st = to_device(host)
         for i in range(k + m):
             if not present[i]:
                 st[:, i].fill_(0)
         enc.ReconstructBatch(st, present)
-        assert np.array_equal(st.cpu().numpy(), host)
+        assert np.array_equal(to_numpy(st), host)
         assert rs.rtc_wait(120_000)
     assert rs.rtc_stats()["failed"] == 0
 
@@ -316,12 +311,12 @@ def test_gpu_network_loaded_once_by_concurrent_launches(knob):
     host = _oracle_stripes(k, m, B, S, 31)
     enc = rs.New(k, m)
     present = rpc_present(k, m, [0, 4, 11])
-    st0 = torch.from_numpy(host).cuda()
+    st0 = to_device(host)
     enc.ReconstructBatch(st0, present)           # requests the network; runs the tables
-    assert np.array_equal(st0.cpu().numpy(), host)
+    assert np.array_equal(to_numpy(st0), host)
     assert rs.rtc_wait(120_000)                  # compiled, not yet loaded
     before = rs.rtc_stats()
-    bufs = [torch.from_numpy(host).cuda() for _ in range(8)]
+    bufs = [to_device(host) for _ in range(8)]
     for b in bufs:
         for i in range(k + m):
             if not present[i]:
@@ -346,7 +341,7 @@ def test_gpu_network_loaded_once_by_concurrent_launches(knob):
         x.join()
     assert not errors, errors
     for b in bufs:
-        assert np.array_equal(b.cpu().numpy(), host)
+        assert np.array_equal(to_numpy(b), host)
     after = rs.rtc_stats()
     assert after["failed"] == before["failed"]
     assert after["loaded"] - before["loaded"] == 1, (before, after)   # one pass, one device
@@ -372,15 +367,15 @@ def test_gpu_network_pointer_table_misaligned_and_ragged(knob):
                 shards.append(torch.empty(0, dtype=torch.uint8, device="cuda"))
             elif i == odd:
                 t = torch.empty(S + 1, dtype=torch.uint8, device="cuda")[1:]
-                t.copy_(torch.from_numpy(host[i]))
+                t.copy_(from_numpy_pinned(host[i]))
                 shards.append(t)
             else:
-                shards.append(torch.from_numpy(host[i]).cuda())
+                shards.append(to_device(host[i]))
         before = rs.rtc_stats()
         enc.Reconstruct(shards)
         torch.cuda.synchronize()
         for i in range(k + m):
-            assert np.array_equal(shards[i].cpu().numpy(), host[i]), (S, odd, i)
+            assert np.array_equal(to_numpy(shards[i]), host[i]), (S, odd, i)
         assert rs.rtc_stats()["failed"] == before["failed"]
 
 

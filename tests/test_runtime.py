@@ -18,6 +18,7 @@ import pytest
 from conftest import ROOT  # noqa: F401
 from blb_amd import _lib
 from blb_amd import reedsolomon as rs
+from blb_amd.hostcopy import to_numpy
 from oracle import rs_numpy as N
 
 MIB = 1 << 20
@@ -140,7 +141,7 @@ def test_device_parts_split_batch(oracle_lib):
     enc = rs.New(k, m)
     enc.EncodeParts(parts)
     torch.cuda.synchronize()
-    host = st.cpu().numpy()
+    host = to_numpy(st)
     for b in range(B):
         ref = _oracle_parity(oracle_lib, k, m, [host[b, i] for i in range(k)])
         for j in range(m):

@@ -23,6 +23,7 @@ import numpy as np
 import pytest
 
 from blb_amd import reedsolomon as rs
+from blb_amd.hostcopy import to_device, to_numpy
 from oracle import rs_numpy as N
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -145,7 +146,7 @@ def test_gpu_wrong_tag_dev_ptrs_recorded_per_device():
     truth = _stripe(k, m, S, 31)
     enc = rs.New(k, m)
     assert rs.table_fault_take(0) is None
-    sh = [torch.from_numpy(truth[i]).cuda() if i < k else torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
+    sh = [to_device(truth[i]) if i < k else torch.full((S,), 0xA5, dtype=torch.uint8, device="cuda")
           for i in range(k + m)]
     rs.debug_corrupt_next_table(k + 2)
     enc.Encode(sh)
@@ -160,7 +161,7 @@ def test_gpu_wrong_tag_dev_ptrs_recorded_per_device():
     torch.cuda.synchronize()
     assert rs.table_fault_take(0) is None
     for i in range(k, k + m):
-        assert np.array_equal(sh[i].cpu().numpy(), truth[i]), i
+        assert np.array_equal(to_numpy(sh[i]), truth[i]), i
 
 
 @pytest.mark.gpu
@@ -171,6 +172,7 @@ def test_gpu_default_recovery_keeps_hiprtc_out_of_the_process():
     code = r'''
 import numpy as np, torch
 from blb_amd import reedsolomon as rs
+from blb_amd.hostcopy import to_device, to_numpy
 from oracle import rs_numpy as N
 k, m, S = 12, 5, 2 * 16384 + 48
 rng = np.random.default_rng(5)
@@ -179,12 +181,12 @@ host = np.stack(data + list(N.encode(k, m, data)))[None]
 present = [i not in (1, 3, 5, 8, 10) for i in range(k + m)]
 enc = rs.New(k, m)
 def run():
-    st = torch.from_numpy(host).cuda()
+    st = to_device(host)
     for i in range(k + m):
         if not present[i]:
             st[:, i].fill_(0)
     enc.ReconstructBatch(st, present)
-    assert np.array_equal(st.cpu().numpy(), host)
+    assert np.array_equal(to_numpy(st), host)
 run()
 assert rs.rtc_stats()["requested"] == 0
 print("MAPS1", "libhiprtc" in open("/proc/self/maps").read())
