@@ -271,10 +271,22 @@ def scale_extras(enc, k, m, S, world, rank, dev, dist):
     lists = [[host[b, i] for i in range(k + m)] for b in range(nb)]
     enc.EncodeHostBatch(lists)
     t_host = timed_all_ranks(lambda: enc.EncodeHostBatch(lists), 2, dev, dist)
+    parity = host[:, k:].copy()
+    # The copy-engine form BASELINE config 5 names: hipMemcpyAsync H2D of the data shards into a
+    # device ring, the kernel on HBM, hipMemcpyAsync D2H of the parity, over nstreams streams.
+    dma = {}
+    for ns in (2, 3, 4):
+        host[:, k:] = 0xA5
+        enc.EncodeHostBatch(lists, nstreams=ns)
+        same = bool(np.array_equal(host[:, k:], parity))
+        t = timed_all_ranks(lambda: enc.EncodeHostBatch(lists, nstreams=ns), 2, dev, dist)
+        dma[f"nstreams_{ns}"] = {"GiBps_data": round(nb * world * k * S * 2 / GIB / t, 2), "parity_same_as_zero_copy": same}
     out["config5_pcie_inclusive_encode"] = {
         "GiBps_data": round(nb * world * k * S * 2 / GIB / t_host, 2), "stripes_per_gpu": nb,
-        "note": "pinned host stripes coded in place over PCIe (zero-copy: data read and parity "
-                "written in host memory by the kernel); not the bench value"}
+        "copy_engines": dma,
+        "note": "pinned host stripes; GiBps_data = coded in place over PCIe (zero copy: data read and "
+                "parity written in host memory by the kernel, the shipped default nstreams = 0); "
+                "copy_engines = hipMemcpyAsync H2D / kernel / D2H pipeline on a device ring; not the bench value"}
     del pinned
     return out
 
@@ -489,22 +501,31 @@ def recovery_extras(S, dev, reps=3):
         for name, present, data_only, nrows in rows:
             targets = [i for i in range(n) if not present[i] and (i < k or not data_only)]
             ref = {i: st[:, i].clone() for i in targets if i < k}
-            for i in targets:
-                st[:, i].fill_(0xA5)
             with rs.tuning(BLBRS_RTC=1):
                 net = rs.rtc_eligible(k, nrows)   # a wide pass: time its opt-in run-time network too
-            with rs.tuning(BLBRS_RTC=2 if net else 0):
-                e.ReconstructBatch(st, present, data_only=data_only)  # compiles and loads the network
-            torch.cuda.synchronize(dev)
-            exact = all(bool(torch.equal(st[:, i], r)) for i, r in ref.items())
-            if not data_only:
-                exact = exact and bool(e.VerifyBatch(st).all())
+            wide = k + nrows > rs.get_tuning("BLBRS_TAB_CHUNKS")   # shipped: chunk-major tables
+            # Bit-exactness of every variant timed below: the shipped default first, then the
+            # opt-in network (compiled and loaded here) and the row-major tables of round 5.
+            knobs = {"shipped": {}}
+            if net:
+                knobs["network"] = {"BLBRS_RTC": 2}
+            if wide:
+                knobs["tables_row_major"] = {"BLBRS_TAB_CHUNKS": 99}
+            exact = {}
+            for key, kn in knobs.items():
+                for i in targets:
+                    st[:, i].fill_(0xA5)
+                with rs.tuning(**kn):
+                    e.ReconstructBatch(st, present, data_only=data_only)
+                torch.cuda.synchronize(dev)
+                ok = all(bool(torch.equal(st[:, i], r)) for i, r in ref.items())
+                if not data_only:
+                    ok = ok and bool(e.VerifyBatch(st).all())
+                exact[key] = ok
             del ref
             u = 4 if k + nrows <= 9 else 2
             run = lambda: e.ReconstructBatch(st, present, data_only=data_only)  # noqa: E731
-            fns = {"shipped": run}
-            if net:
-                fns["network"] = run
+            fns = {key: run for key in knobs}
             if probe is not None:
                 for pu in (1, 2, 4):
                     fns[f"probe_u{pu}"] = (lambda pu=pu: probe.stream_probe(
@@ -512,16 +533,21 @@ def recovery_extras(S, dev, reps=3):
             times = {key: [] for key in fns}
             for _ in range(reps):
                 for key, fn in fns.items():
-                    with rs.tuning(**({"BLBRS_RTC": 2} if key == "network" else {})):
+                    with rs.tuning(**knobs.get(key, {})):
                         times[key].append(_ev_ms(fn, 1, stream, dev))
             e.EncodeBatch(st)  # the probe wrote garbage over parity shards [k, k + rows): restore them
             ms = {key: sorted(v)[len(v) // 2] for key, v in times.items()}
             nbytes = B * (k + nrows) * S
             row = {"rows": nrows, "present": [i for i in range(n) if present[i]], "algorithmic_bytes": nbytes,
                    "ms": round(ms["shipped"], 3), "frac_of_8TBps": round(nbytes / (ms["shipped"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                   "bit_exact": exact}
+                   "bit_exact": exact["shipped"],
+                   "kernel": "tables, chunk-major (TableChunks)" if wide else "tables"}
             if net:  # opt-in (BLBRS_RTC=1/2); the shipped default runs the tables
                 row["network_ms"] = round(ms["network"], 3)
+                row["network_bit_exact"] = exact["network"]
+            if wide:  # round 5's shipped form of the same pass
+                row["tables_row_major_ms"] = round(ms["tables_row_major"], 3)
+                row["tables_row_major_bit_exact"] = exact["tables_row_major"]
             if probe is not None:
                 best = min(ms[f"probe_u{pu}"] for pu in (1, 2, 4))
                 row.update({"probe_ms_same_u": round(ms[f"probe_u{u}"], 3), "probe_ms_best_u": round(best, 3),

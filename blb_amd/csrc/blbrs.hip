@@ -1616,9 +1616,55 @@ int blbrs_verify_parts(blbrs_encoder* enc, const blbrs_dev_part* parts, size_t n
 
 // ---- streaming host path ----
 
+// The copy-engine form of BASELINE config 5 (nstreams >= 1): pinned host stripes -> a device ring
+// -> host parity.  Stripe b goes to slot b % R on stream b % R: hipMemcpyAsync of its k data
+// shards into the slot, rs_code_kernel over the slot (strided, device-resident), hipMemcpyAsync
+// of its m parity shards back.  One stream per slot keeps a slot's reuse in order, and R streams
+// overlap the H2D, kernel and D2H of consecutive stripes (PCIe is full duplex).  Every shard is
+// pinned, device-visible host memory: the library never hands HIP a pageable range to copy
+// (DESIGN §4h); the caller checked.
+static int dma_run(blbrs_encoder* enc, const HostPlan& hp, uint8_t* const* shards, size_t batch, size_t S, int dev,
+                   int nstreams) {
+    const int k = enc->k, n = enc->k + enc->m;
+    const DevPlan* plan = nullptr;
+    int rc = enc->dev_plan("E", hp, dev, &plan);
+    if (rc) return rc;
+    const int R = std::max(1, std::min(nstreams, 8));
+    const size_t pitch = round_up(S, 256), slot = pitch * n;
+    std::vector<hipStream_t> s(R, nullptr);
+    uint8_t* ring = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&ring), slot * static_cast<size_t>(std::min<size_t>(R, batch)));
+    for (int i = 0; i < R && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking);
+    for (size_t b = 0; b < batch && e == hipSuccess; ++b) {
+        const int r = static_cast<int>(b % R);
+        uint8_t* base = ring + static_cast<size_t>(r) * slot;
+        for (int i = 0; i < k && e == hipSuccess; ++i)
+            e = hipMemcpyAsync(base + static_cast<size_t>(i) * pitch, shards[b * n + i], S, hipMemcpyHostToDevice, s[r]);
+        if (e != hipSuccess) break;
+        Stripes st;
+        st.base = base;
+        st.shard_stride = pitch;
+        st.stripe_stride = slot;
+        st.nshards = static_cast<uint32_t>(n);
+        st.aligned = true;
+        if ((rc = run_plan(*plan, st, 1, S, Mode::kStore, nullptr, s[r]))) break;
+        for (int i = k; i < n && e == hipSuccess; ++i)
+            e = hipMemcpyAsync(shards[b * n + i], base + static_cast<size_t>(i) * pitch, S, hipMemcpyDeviceToHost, s[r]);
+    }
+    for (auto& x : s)
+        if (x) {
+            const hipError_t f = hipStreamSynchronize(x);
+            if (e == hipSuccess) e = f;
+            (void)hipStreamDestroy(x);
+        }
+    if (ring) (void)hipFree(ring);
+    if (rc) return rc;
+    return e == hipSuccess ? BLBRS_OK : hip_fail(e, "host batch (copy engines)");
+}
+
 int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch, size_t shard_len,
                             int nstreams) {
-    (void)nstreams;
+    if (nstreams < 0) return fail(BLBRS_ERR_INVALID_ARG, "nstreams must be >= 0");
     if (!enc || !shard_ptrs) return fail(BLBRS_ERR_INVALID_ARG, "NULL argument");
     if (batch == 0 || shard_len == 0) return BLBRS_OK;
     const size_t n = static_cast<size_t>(enc->k + enc->m);
@@ -1650,7 +1696,16 @@ int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size
         ticket.take(p.dev, p.occ, static_cast<uint64_t>(p.count) * n * shard_len);
         rt::DeviceGuard guard;
         p.rc = guard.enter(p.dev);
-        if (p.rc == BLBRS_OK) p.rc = host_run(enc, steps, shard_ptrs + p.start * n, p.count, shard_len, nullptr, p.dev);
+        // nstreams >= 1 and every shard of the part pinned: the copy-engine pipeline; otherwise
+        // the kernels code pinned shards in place and pageable ones are staged by CPU copies.
+        bool dma = nstreams >= 1;
+        for (size_t i = 0; dma && i < p.count * n; ++i) {
+            uint64_t view = 0;
+            int owner = -1;
+            dma = rt::device_view(shard_ptrs[p.start * n + i], &view, &owner) && owner < 0;
+        }
+        if (p.rc == BLBRS_OK && dma) p.rc = dma_run(enc, *hp, shard_ptrs + p.start * n, p.count, shard_len, p.dev, nstreams);
+        else if (p.rc == BLBRS_OK) p.rc = host_run(enc, steps, shard_ptrs + p.start * n, p.count, shard_len, nullptr, p.dev);
         if (p.rc != BLBRS_OK) p.msg = rt::last_error();
     };
     std::vector<std::thread> th;

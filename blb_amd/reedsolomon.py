@@ -447,8 +447,11 @@ class Encoder:
         _check(self._lib.blbrs_verify_parts(self._h, arr, len(parts), S, fp))
         return [f == 0 for f in flags]
 
-    def EncodeHostBatch(self, stripes: Sequence[Sequence[np.ndarray]], nstreams: int = 3) -> None:
-        """Streaming encode of host-resident stripes (pinned memory gives full PCIe rate)."""
+    def EncodeHostBatch(self, stripes: Sequence[Sequence[np.ndarray]], nstreams: int = 0) -> None:
+        """Streaming encode of host-resident stripes (blbrs_encode_host_batch).  nstreams = 0:
+        pinned stripes coded in place over PCIe (zero copy), pageable ones staged by CPU copies;
+        nstreams >= 1: pinned stripes through the copy engines (hipMemcpyAsync H2D, kernel on a
+        device ring, D2H) on that many streams."""
         n = self.Shards
         B = len(stripes)
         if B == 0:

@@ -224,10 +224,16 @@ int blbrs_verify_parts(blbrs_encoder* enc, const blbrs_dev_part* parts, size_t n
 /* ---- streaming host path (host stripes -> GPU -> host parity) ----
  * Encodes `batch` stripes whose k+m shards are HOST pointers (shard_ptrs stripe-major).  The
  * stripes are split contiguously over the encoder's device list, one host thread per entry.
- * Pinned (blbrs_buffer_get / blbrs_host_alloc / blbrs_host_register) stripes are coded in
- * place over PCIe; pageable ones are staged through a stream worker (H2D, kernel and D2H of
- * successive column chunks overlapped on its two streams).  nstreams is kept for ABI
- * compatibility and ignored. */
+ * nstreams = 0 (the default of the language bindings): pinned (blbrs_buffer_get /
+ * blbrs_host_alloc / blbrs_host_register) stripes are coded in place, the kernels reading the
+ * data and writing the parity over PCIe (zero copy).  Pageable stripes are staged by CPU copies
+ * through the worker's pinned, device-mapped buffer, in column chunks, so the CPU copies of one
+ * chunk overlap the kernels of the next; no pageable memory is handed to a HIP copy.
+ * nstreams >= 1 (at most 8 used): when every shard of a device's part is pinned, that part runs
+ * the copy-engine pipeline instead: hipMemcpyAsync of each stripe's k data shards into a device
+ * ring slot, the kernel on the slot, hipMemcpyAsync of its m parity shards back, stripe b on
+ * stream b % nstreams.  Parts with pageable shards take the staged path above.
+ * INVALID_ARG for nstreams < 0. */
 int blbrs_encode_host_batch(blbrs_encoder* enc, uint8_t* const* shard_ptrs, size_t batch,
                             size_t shard_len, int nstreams);
 
@@ -455,7 +461,7 @@ int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t s
 /* ---- A/B knobs and run-time networks ---- */
 
 /* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_EC_PERSISTENT, BLBRS_RTC,
- * BLBRS_RTC_WIDE; blb_amd/csrc/tuning.hpp), each a choice between shipped policies,
+ * BLBRS_RTC_WIDE, BLBRS_TAB_CHUNKS; blb_amd/csrc/tuning.hpp), each a choice between shipped policies,
  * start from the environment, read once, and change only here -- never by setenv while the
  * library runs.  INVALID_ARG for an unknown name. */
 int blbrs_set_tuning(const char* name, long value);

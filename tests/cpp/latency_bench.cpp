@@ -231,6 +231,44 @@ int main(int argc, char** argv) {
         if (std::memcmp(got, s.piece[target], L)) ++bad;
         print("steady_state", threads == 0 ? "gpu" : "cpu", threads, L, dist(t));
     }
+    // Cold inputs: every call reads a stripe (and writes an output) last touched long before --
+    // a ring of distinct stripes larger than the host's last-level cache, visited in order --
+    // as replies fresh off the network are for the CPU's caches (round 6).
+    // The steady-state rows above reuse one stripe, so the CPU side runs cache-hot there.
+    {
+        constexpr size_t kColdBytes = size_t{768} << 20;  // > the 256 MB L3 of the box's EPYC 9575F
+        const size_t per = static_cast<size_t>(6 + 3 + 1) * L;
+        const int nring = static_cast<int>(std::clamp<size_t>(kColdBytes / per + 1, 8, 20000));
+        std::vector<Stripe*> ring;
+        std::vector<uint8_t*> outs;
+        for (int i = 0; i < nring; ++i) {
+            ring.push_back(new Stripe(6, 3, L, rng));
+            outs.push_back(static_cast<uint8_t*>(std::aligned_alloc(64, (L + 63) / 64 * 64)));
+            std::memset(outs.back(), 0, L);
+        }
+        const int creps = std::min(reps, 4 * nring);
+        for (int side = 0; side < 2; ++side) {
+            std::vector<double> t;
+            t.reserve(creps);
+            for (int r = 0; r < creps; ++r) {
+                const Stripe& cs = *ring[r % nring];
+                uint8_t* o = outs[r % nring];
+                if (side == 0) {
+                    t.push_back(gpu_call(cs, present, target, o));
+                } else {
+                    const auto t0 = Clock::now();
+                    cpu_call(cs, present, target, o, 1);
+                    t.push_back(us_since(t0));
+                }
+                if (r < nring && std::memcmp(o, cs.piece[target], L)) ++bad;
+            }
+            print("steady_state_cold_inputs", side == 0 ? "gpu" : "cpu", side == 0 ? 0 : 1, L, dist(t));
+        }
+        std::printf("{\"row\": \"cold_ring\", \"piece_bytes\": %zu, \"stripes\": %d, \"ring_bytes\": %zu}\n", L, nring,
+                    static_cast<size_t>(nring) * per);
+        for (auto* x : ring) delete x;
+        for (auto* o : outs) std::free(o);
+    }
     std::printf("{\"row\": \"check\", \"piece_bytes\": %zu, \"mismatches\": %d, \"inputs\": \"%s\"}\n", L, bad,
                 L > kSmallMax ? "pool (pinned)" : "pageable");
     return bad ? 2 : 0;

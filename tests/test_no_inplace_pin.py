@@ -86,6 +86,11 @@ mark("EncodeHostBatch")
 stripes = [[d.copy() for d in data] + [np.empty(S, np.uint8) for _ in range(m)] for _ in range(2)]
 enc.EncodeHostBatch(stripes)
 assert np.array_equal(stripes[1][6], full[6])
+mark("EncodeHostBatch copy engines")  # pinned stripes through hipMemcpyAsync (nstreams >= 1)
+pin = torch.empty((2, k + m, S), dtype=torch.uint8).pin_memory().numpy()
+pin[:, :k] = np.stack(data)
+enc.EncodeHostBatch([[pin[b, i] for i in range(k + m)] for b in range(2)], nstreams=3)
+assert np.array_equal(pin[1, 7], full[7])
 mark("Checksum")
 buf = rng.integers(0, 256, 8 * S + 13, dtype=np.uint8)
 checksum.Checksum(buf, 65532)

@@ -14,7 +14,7 @@
 #            rocprof      rocprofv3 --kernel-trace --stats of bench.py --steps 10 --no-extra
 #            ab:CMD       an A/B or measurement driver, e.g. "ab:tools/rpc_shapes.py --reps 5"
 #            probe:ARGS   tools/_build/mix_probe ARGS
-#            latency      tests/cpp/_build/latency_bench at 4 KiB, 64 KiB, 1 MiB, 8 MiB -> latency.jsonl
+#            latency      tests/cpp/_build/latency_bench at 4 KiB .. 8 MiB -> latency.jsonl
 #            crcab        tools/crc_pmc.sh: CRC load-path A/B with FETCH_SIZE (variants from crc_variants.sh)
 # e.g. gpurun -- 'bash tools/gpu_round.sh r4val tests,smoke,bench,rocprof'
 set -o pipefail
@@ -54,7 +54,7 @@ for step in "${LIST[@]}"; do
       timeout -k 10 900 python -u ${step#ab:} > "$OUT/ab_$n.jsonl" 2> "$OUT/ab_$n.err"
       rc=$?; cut -c1-3000 "$OUT/ab_$n.jsonl"; tail -3 "$OUT/ab_$n.err" ;;
     latency)
-      for L in 4096 65536 1048576 8388608; do
+      for L in 4096 65536 262144 1048576 2097152 4194304 8388608; do
         timeout -k 10 300 tests/cpp/_build/latency_bench $L >> "$OUT/latency.jsonl" 2>> "$OUT/latency.err" || { rc=$?; break; }
         rc=0
       done

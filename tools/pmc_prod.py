@@ -16,9 +16,12 @@ the same process:
   pack_tracts       PackPieces of B 8 MiB pieces from distinct tract sources (pack_kernel)
   pack_encode_rs6_3_distinct  PackEncode of all B*k data pieces, distinct sources (pack_encode_kernel)
   pack_encode_rs8_3_distinct  the same at RS(8,3) B=512
-  then RS(12,5) B=512: EncodeBatch and EncodeBatchCRC(65532) on the compiled network, a
-  VerifyBatch, and blb's recovery RPC shape (data shard 1 bad, the first 12 good pieces read,
-  all 5 absent slots rebuilt) on its run-time network (BLBRS_RTC = 2: compiled by the warm-up).
+  then RS(12,5) B=480 (the bench's recovery batch): EncodeBatch and EncodeBatchCRC(65532) on the
+  compiled network, a VerifyBatch, and blb's recovery shapes with the shipped default knobs
+  (chunk-major v_perm tables, rs_code.hpp TableChunks): the RPC with 1 and 5 bad data pieces (the
+  first 12 good pieces read, all 5 absent slots rebuilt) and the client's 5-row ReconstructData;
+  then the same 1-bad RPC on round 5's row-major tables (BLBRS_TAB_CHUNKS = 99) and on its
+  opt-in run-time network (BLBRS_RTC = 2: compiled by the warm-up).
 
 Prints the op plan (label, kernel-name needle, launches) and the libblbrs.so sha256 as one
 JSON line; the summary consumes dispatches op by op in that order."""
@@ -70,7 +73,6 @@ torch.cuda.synchronize()
 del src, dst
 torch.cuda.empty_cache()
 
-rs.set_tuning("BLBRS_RTC", 2)
 st = torch.empty((B, k + m, S), dtype=torch.uint8, device=dev)
 g = torch.Generator(device=dev)
 g.manual_seed(97531)
@@ -132,7 +134,7 @@ torch.cuda.empty_cache()
 
 # blb's widest class: encode and encode fused with the ChecksumFile CRCs on the compiled
 # bit-plane network, verify, and the recovery RPC shape on its run-time network.
-k2, m2, B2 = 12, 5, 512
+k2, m2, B2 = 12, 5, 480
 n2 = k2 + m2
 st = torch.empty((B2, n2, S), dtype=torch.uint8, device=dev)
 st[:, :k2].random_(0, 256, generator=g)
@@ -143,10 +145,28 @@ op("encode_rs12_5_network", "rs_code_kernel", lambda: enc2.EncodeBatch(st), wb)
 op("encode_crc_rs12_5_network", "encode_crc_tile_kernel", lambda: enc2.EncodeBatchCRC(st, 65532), wb)
 oks2 = []
 op("verify_rs12_5_network", "rs_code_kernel", lambda: oks2.append(enc2.VerifyBatch(st)), wb)
-rpc_present = [i != 1 and i <= k2 for i in range(n2)]  # first 12 good pieces: 0, 2..12
-op("rpc_1bad_rs12_5_rtc_network", "rs_code_kernel", lambda: enc2.ReconstructBatch(st, rpc_present), wb,
-   present=[i for i in range(n2) if rpc_present[i]])
-ok2 = bool(enc2.VerifyBatch(st).all()) and bool(oks2[-1].all())
+spread = [1 + (i * k2) // m2 for i in range(m2)]   # bench.py recovery_extras' bad pieces
+
+
+def first_k_good(bad):
+    good = [i for i in range(n2) if i not in bad]
+    return [i in good[:k2] for i in range(n2)]
+
+
+rpc1, rpc5 = first_k_good(spread[:1]), first_k_good(spread)
+ok2 = bool(oks2[-1].all())
+for label, present, data_only, rows in (("rpc_1bad_rs12_5", rpc1, False, m2), ("rpc_5bad_rs12_5", rpc5, False, m2),
+                                        ("client_rows5_rs12_5", rpc5, True, m2)):
+    op(label, "rs_code_kernel", lambda p=present, d=data_only: enc2.ReconstructBatch(st, p, data_only=d),
+       B2 * (k2 + rows) * S, present=[i for i in range(n2) if present[i]], knobs="shipped default (TableChunks)")
+    ok2 = ok2 and bool(check(f"verify_after_{label}", "rs_code_kernel", lambda: enc2.VerifyBatch(st)).all())
+with rs.tuning(BLBRS_TAB_CHUNKS=99):
+    op("rpc_1bad_rs12_5_tables_row_major", "rs_code_kernel", lambda: enc2.ReconstructBatch(st, rpc1), wb,
+       present=[i for i in range(n2) if rpc1[i]], knobs="BLBRS_TAB_CHUNKS=99")
+with rs.tuning(BLBRS_RTC=2):
+    op("rpc_1bad_rs12_5_rtc_network", "rs_code_kernel", lambda: enc2.ReconstructBatch(st, rpc1), wb,
+       present=[i for i in range(n2) if rpc1[i]], knobs="BLBRS_RTC=2")
+ok2 = ok2 and bool(enc2.VerifyBatch(st).all())
 lib = _lib.LIB_PATH
 print(json.dumps({"lib": lib, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
                   "verify_ok": verify_ok, "k": k, "m": m, "batch": B, "shard": S, "reps": REPS, "plan": plan,

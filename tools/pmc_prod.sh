@@ -13,5 +13,6 @@ run() {  # name counters...
 run fetch FETCH_SIZE \
 && run write WRITE_SIZE \
 && run sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS \
+&& run sq2 SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD \
 && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o trace -- python3 tools/pmc_prod.py > $out/trace.log 2>&1 \
 && python3 tools/pmc_prod_summary.py $out $tag $commit

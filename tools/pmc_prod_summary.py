@@ -53,6 +53,7 @@ def main():
     fetch = dispatches(rows(csv_in(out, "fetch", "counter_collection")))
     write = dispatches(rows(csv_in(out, "write", "counter_collection")))
     sq = dispatches(rows(csv_in(out, "sq", "counter_collection")))
+    sq2 = dispatches(rows(csv_in(out, "sq2", "counter_collection"))) if os.path.isdir(os.path.join(out, "sq2")) else None
     trace = sorted(rows(csv_in(out, "trace", "kernel_trace")), key=lambda r: int(r["Dispatch_Id"]))
 
     # calibration: the copy kernel that follows the fill (both 8 GiB)
@@ -81,6 +82,7 @@ def main():
     f_ops = consume(fetch, lambda x: x[1], meta["plan"])
     w_ops = consume(write, lambda x: x[1], meta["plan"])
     s_ops = consume(sq, lambda x: x[1], meta["plan"])
+    s2_ops = consume(sq2, lambda x: x[1], meta["plan"]) if sq2 else {}
     t_ops = consume(trace, lambda r: r["Kernel_Name"], meta["plan"])
 
     def mean(vals):
@@ -95,6 +97,12 @@ def main():
         wr = mean([x[2]["WRITE_SIZE"] for x in w_ops[label]]) * 1024.0 * w_scale
         counters = sorted({c for x in s_ops[label] for c in x[2]})
         sqv = {c: mean([x[2].get(c, 0.0) for x in s_ops[label]]) for c in counters}
+        # the second SQ pass (wait and issue counters): its own SQ_WAVES / SQ_WAVE_CYCLES
+        # normalise its counters, so they are kept apart under "sq2"
+        sq2v = None
+        if s2_ops:
+            c2 = sorted({c for x in s2_ops[label] for c in x[2]})
+            sq2v = {c: mean([x[2].get(c, 0.0) for x in s2_ops[label]]) for c in c2}
         ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in t_ops[label]]
         e = {"kernel": f_ops[label][0][1], "launches_averaged": len(ms),
              "hbm_read_bytes": round(rd), "hbm_write_bytes": round(wr),
@@ -105,6 +113,16 @@ def main():
             e["lds_bank_conflict_frac"] = round(sqv.get("SQ_LDS_BANK_CONFLICT", 0) / sqv["SQ_LDS_IDX_ACTIVE"], 4)
         if sqv.get("SQ_WAVES"):
             e["valu_insts_per_wave"] = round(sqv.get("SQ_INSTS_VALU", 0) / sqv["SQ_WAVES"], 1)
+        if sq2v:
+            e["sq2"] = sq2v
+            if sq2v.get("SQ_WAVE_CYCLES"):
+                wc = sq2v["SQ_WAVE_CYCLES"]
+                e["wait_inst_any_frac_of_wave_cycles"] = round(sq2v.get("SQ_WAIT_INST_ANY", 0) / wc, 4)
+                e["wait_any_frac_of_wave_cycles"] = round(sq2v.get("SQ_WAIT_ANY", 0) / wc, 4)
+                e["active_valu_frac_of_wave_cycles"] = round(sq2v.get("SQ_ACTIVE_INST_VALU", 0) / wc, 4)
+            if sq2v.get("SQ_WAVES"):
+                e["salu_insts_per_wave"] = round(sq2v.get("SQ_INSTS_SALU", 0) / sq2v["SQ_WAVES"], 1)
+                e["smem_insts_per_wave"] = round(sq2v.get("SQ_INSTS_SMEM", 0) / sq2v["SQ_WAVES"], 1)
         kernels[label] = e
     k, m, B, S = meta["k"], meta["m"], meta["batch"], meta["shard"]
     wide = meta.get("wide")

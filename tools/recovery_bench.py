@@ -17,4 +17,4 @@ for arg in sys.argv[1:]:
     rs.set_tuning(name, int(value))
 dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
-print(json.dumps(bench.recovery_extras(bench.TRACT, dev)))
+print(json.dumps(bench.recovery_extras(bench.TRACT, dev, reps=int(os.environ.get("REPS", "3")))))
