@@ -461,7 +461,7 @@ def _stream_probe():
     return lib
 
 
-def recovery_extras(S, dev, reps=3):
+def recovery_extras(S, dev, reps=3, classes=((6, 3, 1024), (8, 3, 768), (10, 3, 640), (12, 5, 480))):
     """blb's real recovery call shapes for every storage class (rank 0 at N=1), B chosen so each
     batch is ~64-72 GiB of HBM:
 
@@ -481,7 +481,7 @@ def recovery_extras(S, dev, reps=3):
     probe = _stream_probe()
     stream = torch.cuda.current_stream(dev)
     out = {"note": "ms = median of interleaved reps; probe = trivial-XOR stream, same bytes/layout/launch"}
-    for k, m, B in ((6, 3, 1024), (8, 3, 768), (10, 3, 640), (12, 5, 480)):
+    for k, m, B in classes:
         n = k + m
         st = torch.empty((B, n, S), dtype=torch.uint8, device=dev)
         g = torch.Generator(device=dev)
@@ -503,14 +503,11 @@ def recovery_extras(S, dev, reps=3):
             ref = {i: st[:, i].clone() for i in targets if i < k}
             with rs.tuning(BLBRS_RTC=1):
                 net = rs.rtc_eligible(k, nrows)   # a wide pass: time its opt-in run-time network too
-            wide = k + nrows > rs.get_tuning("BLBRS_TAB_CHUNKS")   # shipped: chunk-major tables
-            # Bit-exactness of every variant timed below: the shipped default first, then the
-            # opt-in network (compiled and loaded here) and the row-major tables of round 5.
+            # Bit-exactness of every variant timed below: the shipped default (tables) first, then
+            # the opt-in network (compiled and loaded here).
             knobs = {"shipped": {}}
             if net:
                 knobs["network"] = {"BLBRS_RTC": 2}
-            if wide:
-                knobs["tables_row_major"] = {"BLBRS_TAB_CHUNKS": 99}
             exact = {}
             for key, kn in knobs.items():
                 for i in targets:
@@ -540,14 +537,10 @@ def recovery_extras(S, dev, reps=3):
             nbytes = B * (k + nrows) * S
             row = {"rows": nrows, "present": [i for i in range(n) if present[i]], "algorithmic_bytes": nbytes,
                    "ms": round(ms["shipped"], 3), "frac_of_8TBps": round(nbytes / (ms["shipped"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                   "bit_exact": exact["shipped"],
-                   "kernel": "tables, chunk-major (TableChunks)" if wide else "tables"}
+                   "bit_exact": exact["shipped"]}
             if net:  # opt-in (BLBRS_RTC=1/2); the shipped default runs the tables
                 row["network_ms"] = round(ms["network"], 3)
                 row["network_bit_exact"] = exact["network"]
-            if wide:  # round 5's shipped form of the same pass
-                row["tables_row_major_ms"] = round(ms["tables_row_major"], 3)
-                row["tables_row_major_bit_exact"] = exact["tables_row_major"]
             if probe is not None:
                 best = min(ms[f"probe_u{pu}"] for pu in (1, 2, 4))
                 row.update({"probe_ms_same_u": round(ms[f"probe_u{u}"], 3), "probe_ms_best_u": round(best, 3),

@@ -256,15 +256,6 @@ __device__ __forceinline__ void code_tile_slow(const CodeArgs& a, uint32_t b, ui
 template <class T> struct is_void { static constexpr bool value = false; };
 template <> struct is_void<void> { static constexpr bool value = true; };
 
-// NET = TableChunks: the v_perm table path, one 16-byte chunk (u) of every input at a time
-// instead of all U at once (store mode, wide shapes).  The loads are the same (all issued
-// up front, chunk-major), but the accumulators and bit groups of one chunk are live instead of
-// U chunks': RS(12,5) at U = 2 from 207 VGPRs (2 waves per SIMD) to <= 168 (3 waves), at the
-// price of re-reading each coefficient's 5 scalar table words per chunk.
-struct TableChunks {};
-template <class T> struct is_table_chunks { static constexpr bool value = false; };
-template <> struct is_table_chunks<TableChunks> { static constexpr bool value = true; };
-
 // BLBRS_NET_WPE > 0: network kernels of k + rows <= 14 ask the compiler for that many waves per
 // SIMD (RS(10,x) networks otherwise land at 129-130 VGPRs, one over the 4-wave budget).  Off in
 // the library build; run-time networks take it from the knob BLBRS_RTC_WPE (rtc.hip).
@@ -273,23 +264,11 @@ template <> struct is_table_chunks<TableChunks> { static constexpr bool value = 
 #endif
 constexpr int net_wpe(int k, int rows, bool cm) { return cm && BLBRS_NET_WPE > 0 && k + rows <= 14 ? BLBRS_NET_WPE : 1; }
 
-// The chunk-major table kernel asks for 3 waves per SIMD (<= 168 VGPRs): left alone the strided
-// RS(12,5) instantiation lands at 182 (2 waves), the pointer-table one at 152.
-#ifndef BLBRS_TC_WPE
-#define BLBRS_TC_WPE 3
-#endif
-template <class NET>
-constexpr int kernel_wpe(int k, int rows) {
-    return is_table_chunks<NET>::value ? BLBRS_TC_WPE : net_wpe(k, rows, !is_void<NET>::value);
-}
-
 template <int K, int MR, int MODE, int ADDR, int U, int NT, class NET = void>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kernel_wpe<NET>(K, MR))))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(net_wpe(K, MR, !is_void<NET>::value))))
 void rs_code_kernel(CodeArgs a) {
-    constexpr bool TC = is_table_chunks<NET>::value;
-    constexpr bool CM = !is_void<NET>::value && !TC;
+    constexpr bool CM = !is_void<NET>::value;
     static_assert(!CM || (K > 0 && U % 2 == 0), "network shapes");
-    static_assert(!TC || (K > 0 && MODE == 0), "chunk-major table path: store mode, compiled k");
     constexpr uint32_t kTile = kTileBytes * U;
     const uint32_t total = a.B * a.tiles_per_stripe;
     const int nr = a.rows;
@@ -394,38 +373,6 @@ void rs_code_kernel(CodeArgs a) {
                     }
                     }
                 }
-            } else if constexpr (TC) {
-                // Chunk-major loads (chunk 0 of every input first), all issued before any math, so
-                // chunk 0's multiply starts while chunk 1 is in flight.
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int c = 0; c < K; ++c) x[c][u] = ld16<NT>(shard_ptr<ADDR>(a, b, in_idx[c]) + lane_off + u * kStep);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    cu32 tu = as_const(a.tables);  // per chunk: the scalar table loads stay in the loop
-                    asm volatile("" : "+s"(tu));
-                    uint32_t au[MR][4] = {};
-#pragma unroll
-                    for (int c = 0; c + 1 < K; c += 2) {
-                        uint32_t xa[4], xb[4];
-                        unpack(x[c][u], xa);
-                        unpack(x[c + 1][u], xb);
-                        madd2<MR, 4>(Groups<4>(xa), [&](int r) { return tu + (r * K + c) * 5; },
-                                     Groups<4>(xb), [&](int r) { return tu + (r * K + c + 1) * 5; }, au, nr);
-                    }
-                    if constexpr (K & 1) {
-                        uint32_t xv[4];
-                        unpack(x[K - 1][u], xv);
-                        madd<MR, 4>(Groups<4>(xv), [&](int r) { return tu + (r * K + K - 1) * 5; }, au, nr);
-                    }
-#pragma unroll
-                    for (int r = 0; r < MR; ++r) {
-                        if (r >= nr) break;
-                        st16<NT>(shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off + u * kStep, pack(au[r]));
-                    }
-                }
             } else {
 #pragma unroll
             for (int c = 0; c < K; ++c) {
@@ -479,8 +426,8 @@ void rs_code_kernel(CodeArgs a) {
         for (int r = 0; r < MR; ++r) {
             if (r >= nr) break;
             uint8_t* q = shard_ptr<ADDR>(a, b, out_idx[r]) + lane_off;
-            if ((CM && MODE == 0 && BLBRS_CM_GROUP_LOADS) || TC) {
-                // stored per group / per chunk above
+            if (CM && MODE == 0 && BLBRS_CM_GROUP_LOADS) {
+                // stored per group above
             } else if (MODE == 0 || (MODE == 2 && r < a.nstore)) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) st16<NT>(q + u * kStep, pack(acc[r] + 4 * u));

@@ -43,10 +43,6 @@ constexpr int pick_u(int K, int MR, int MODE) {
 }
 
 
-// Shapes the chunk-major table kernel is compiled for (k + rows > this); the knob
-// BLBRS_TAB_CHUNKS picks among them.
-constexpr int kTabChunksMin = 13;
-
 template <int K, int MR, int MODE, int ADDR>
 constexpr KernelFn fn_of() { return rs_code_kernel<K, MR, MODE, ADDR, pick_u(K, MR, MODE), kNT>; }
 
@@ -63,11 +59,6 @@ Choice choice_of(bool cm) {
     constexpr int UC = network_u(K, MR, MODE);
     if constexpr (K > 0 && MODE != 2) {
         if (cm) return {rs_code_kernel<K, MR, MODE, ADDR, UC, kNT, bs::EncodeNet<K>>, UC, true, true};
-    }
-    // Wide store passes on tables: one chunk at a time (fewer live registers, one more wave per SIMD).
-    if constexpr (K > 0 && MODE == 0 && K + MR > kTabChunksMin) {
-        if (K + MR > tune::get(tune::kTabChunks))
-            return {rs_code_kernel<K, MR, 0, ADDR, pick_u(K, MR, 0), kNT, code::TableChunks>, pick_u(K, MR, 0), true, false};
     }
     return {fn_of<K, MR, MODE, ADDR>(), pick_u(K, MR, MODE), K > 0, false};
 }

@@ -18,7 +18,6 @@ struct Def {
 // Order = enum Knob.
 constexpr Def kDefs[kCount] = {
     {"BLBRS_BITSLICE", 1}, {"BLBRS_EC_PERSISTENT", 0}, {"BLBRS_RTC", 0}, {"BLBRS_RTC_WIDE", 13},
-    {"BLBRS_TAB_CHUNKS", 13},
 };
 
 // The environment is read once, here (thread-safe static initialisation).

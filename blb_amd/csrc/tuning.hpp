@@ -21,8 +21,6 @@ enum Knob : int {
                      // background, 2 = compiled by the caller (rtc.hpp)
     kRtcWide,        // BLBRS_RTC_WIDE: a decode pass takes a network when k + rows > this (13: RS(12,5)-wide
                      // passes, where the tables are VALU-bound; narrower ones measured +-1-3 %)
-    kTabChunks,      // BLBRS_TAB_CHUNKS: table store passes with k + rows > this (and > 13, the widest
-                     // compiled) take the chunk-major form (rs_code.hpp TableChunks); 99 = never
     kCount
 };
 

@@ -461,7 +461,7 @@ int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t s
 /* ---- A/B knobs and run-time networks ---- */
 
 /* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_EC_PERSISTENT, BLBRS_RTC,
- * BLBRS_RTC_WIDE, BLBRS_TAB_CHUNKS; blb_amd/csrc/tuning.hpp), each a choice between shipped policies,
+ * BLBRS_RTC_WIDE; blb_amd/csrc/tuning.hpp), each a choice between shipped policies,
  * start from the environment, read once, and change only here -- never by setenv while the
  * library runs.  INVALID_ARG for an unknown name. */
 int blbrs_set_tuning(const char* name, long value);

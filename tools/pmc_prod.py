@@ -18,10 +18,9 @@ the same process:
   pack_encode_rs8_3_distinct  the same at RS(8,3) B=512
   then RS(12,5) B=480 (the bench's recovery batch): EncodeBatch and EncodeBatchCRC(65532) on the
   compiled network, a VerifyBatch, and blb's recovery shapes with the shipped default knobs
-  (chunk-major v_perm tables, rs_code.hpp TableChunks): the RPC with 1 and 5 bad data pieces (the
-  first 12 good pieces read, all 5 absent slots rebuilt) and the client's 5-row ReconstructData;
-  then the same 1-bad RPC on round 5's row-major tables (BLBRS_TAB_CHUNKS = 99) and on its
-  opt-in run-time network (BLBRS_RTC = 2: compiled by the warm-up).
+  (the v_perm table kernel): the RPC with 1 and 5 bad data pieces (the first 12 good pieces
+  read, all 5 absent slots rebuilt) and the client's 5-row ReconstructData; then the same 1-bad
+  RPC on its opt-in run-time network (BLBRS_RTC = 2: compiled by the warm-up).
 
 Prints the op plan (label, kernel-name needle, launches) and the libblbrs.so sha256 as one
 JSON line; the summary consumes dispatches op by op in that order."""
@@ -158,11 +157,8 @@ ok2 = bool(oks2[-1].all())
 for label, present, data_only, rows in (("rpc_1bad_rs12_5", rpc1, False, m2), ("rpc_5bad_rs12_5", rpc5, False, m2),
                                         ("client_rows5_rs12_5", rpc5, True, m2)):
     op(label, "rs_code_kernel", lambda p=present, d=data_only: enc2.ReconstructBatch(st, p, data_only=d),
-       B2 * (k2 + rows) * S, present=[i for i in range(n2) if present[i]], knobs="shipped default (TableChunks)")
+       B2 * (k2 + rows) * S, present=[i for i in range(n2) if present[i]], knobs="shipped default (tables)")
     ok2 = ok2 and bool(check(f"verify_after_{label}", "rs_code_kernel", lambda: enc2.VerifyBatch(st)).all())
-with rs.tuning(BLBRS_TAB_CHUNKS=99):
-    op("rpc_1bad_rs12_5_tables_row_major", "rs_code_kernel", lambda: enc2.ReconstructBatch(st, rpc1), wb,
-       present=[i for i in range(n2) if rpc1[i]], knobs="BLBRS_TAB_CHUNKS=99")
 with rs.tuning(BLBRS_RTC=2):
     op("rpc_1bad_rs12_5_rtc_network", "rs_code_kernel", lambda: enc2.ReconstructBatch(st, rpc1), wb,
        present=[i for i in range(n2) if rpc1[i]], knobs="BLBRS_RTC=2")
