@@ -275,7 +275,7 @@ def scale_extras(enc, k, m, S, world, rank, dev, dist):
     # The copy-engine form BASELINE config 5 names: hipMemcpyAsync H2D of the data shards into a
     # device ring, the kernel on HBM, hipMemcpyAsync D2H of the parity, over nstreams streams.
     dma = {}
-    for ns in (2, 3, 4):
+    for ns in (2, 4, 8):
         host[:, k:] = 0xA5
         enc.EncodeHostBatch(lists, nstreams=ns)
         same = bool(np.array_equal(host[:, k:], parity))
