@@ -3,9 +3,9 @@
 HIP copies a pageable source or destination larger than 1 MiB by locking the caller's pages in
 place for the DMA (hsa_amd_memory_lock_to_pool over the page-rounded range; AMD_LOG_LEVEL=4
 logs "Locking to pool ... memFlags = 0x8h" then "HSA Copy Using Pinned resource",
-profiles/r06/fault/).  Every GPU memory fault of rounds 4-5 was raised in such a copy made by
-test code (torch's .cuda() / .cpu() of a 1.4 MB heap array, tests/test_rtc.py), and the library
-itself never takes that path: its host calls stage pageable shards by CPU copies into pinned,
+profiles/r06/fault/).  Every GPU memory fault of round 5 whose log survives was raised in
+such a copy made by test code (torch's .cuda() / .cpu() of a 1.4 MB heap array,
+tests/test_rtc.py), and the library itself never takes that path: its host calls stage pageable shards by CPU copies into pinned,
 device-mapped buffers (blbrs.hip host_run).  These helpers give the Python side the same rule:
 numpy data goes through a pinned torch tensor (hipHostMalloc memory, which HIP copies with no
 lock), in both directions.  tests/test_no_inplace_pin.py checks the rule from HIP's own log.

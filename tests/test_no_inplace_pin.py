@@ -1,7 +1,8 @@
 """No library path and no test helper has HIP lock pageable memory in place.
 
-Every GPU memory fault of rounds 4-5 (r4v2, r4i, r5a, r5i, r5m, r5w, r5y) was raised by a copy that
-HIP made by locking the caller's pageable pages in place: torch's .cuda() (tests/test_rtc.py, r5i,
+Every GPU memory fault of round 5 whose log survives (r5a, r5i, r5m, r5w, r5y; round 4's r4v2 and
+r4i struck at the same point of the suite) was raised by a copy that HIP made by locking the
+caller's pageable pages in place: torch's .cuda() (tests/test_rtc.py, r5i,
 r5m, r5w) or .cpu() (r5a, r5y) of a 1.4 MB heap array.  HIP takes that path for a pageable copy
 larger than 1 MiB (hsa_amd_memory_lock_to_pool over the page-rounded range); AMD_LOG_LEVEL=4 names
 it with "HSA Copy Using Pinned resource" (rocblit.cpp), right after "Locking to pool ... memFlags =
