@@ -1,8 +1,9 @@
 import os
 import sys
 
-# No GPU_PINNED_MIN_XFER_SIZE override (round 6).  Rounds 4-5's intermittent device fault was
-# raised in copies that HIP made by locking pageable test arrays in place (torch .cuda() / .cpu()
+# No GPU_PINNED_MIN_XFER_SIZE override (round 6).  Round 5's intermittent device fault was
+# raised (in every run whose log survives) in copies that HIP made by locking pageable test
+# arrays in place (torch .cuda() / .cpu()
 # of 1.4 MB heap arrays); round 5 hid it by making HIP stage every pageable copy.
 # The test code now moves numpy data through pinned tensors (blb_amd/hostcopy.py), as the
 # library always does, and tests/test_no_inplace_pin.py checks from HIP's log that neither takes
