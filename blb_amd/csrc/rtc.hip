@@ -159,7 +159,8 @@ std::mutex& comgr_mu() {
 }
 
 // hipRTC, opened on first use (dlopen), not linked: a process that never asks for a run-time
-// network -- the default, BLBRS_RTC = 0 -- never maps hipRTC or the LLVM (comgr) it loads.
+// network (no RS(12,5)-wide multi-row pass, or BLBRS_RTC = 0) never maps hipRTC or the LLVM
+// (comgr) it loads.
 struct Hiprtc {
     decltype(&hiprtcCreateProgram) create = nullptr;
     decltype(&hiprtcAddNameExpression) add_name = nullptr;

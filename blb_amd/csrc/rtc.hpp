@@ -11,11 +11,15 @@
 // the kernel next to the pass's tables -- the counterpart of klauspost's inversion tree, one
 // level further: a compiled kernel per cached inverse.
 //
-// Off by default (knob BLBRS_RTC = 0, round 5): the gain is RS(12,5)-wide recovery passes only
-// (2-5 % in the driver's bench), and a run-time compiler brings LLVM into blb's tractserver and
-// client processes; an illegal-address fault seen twice in round 4 while modules were loaded off
-// the launching thread has no pinned cause.  hipRTC is opened with dlopen on the
-// first request, never linked, so a process that does not opt in never maps it or comgr.
+// On by default again since round 6 (knob BLBRS_RTC = 1; off in round 5).  Only RS(12,5)-wide
+// multi-row passes take a network (k + rows > BLBRS_RTC_WIDE = 13, rows >= 2): blb's recovery
+// RPC and the client's multi-row ReconstructData at its widest class.  There the v_perm table
+// kernel keeps the SIMD's VALU ~97 % busy, and under sustained load it fell to 1.05-1.07x of the
+// trivial-XOR stream, while the network stayed within 0.99-1.01x in every process measured
+// (DESIGN §4h, round 6).  The device fault once suspected of module loads was raised by HIP's
+// in-place lock of pageable test arrays, in every round-5 run whose log survives.
+// hipRTC is opened with dlopen on the first request, never linked, so a process that never runs
+// such a pass (or sets BLBRS_RTC = 0) never maps it or comgr.
 // BLBRS_RTC = 1 compiles on a background thread: the pass keeps the table kernel until its
 // network is compiled, so no call waits on the compiler.  That thread makes no HIP call (hipRTC
 // is host-only); the code object is loaded (hipModuleLoadData) by the next launch that wants it,

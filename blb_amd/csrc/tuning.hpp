@@ -17,8 +17,8 @@ enum Knob : int {
     kBitslice = 0,   // BLBRS_BITSLICE: compiled encode network 0 = never, 1 = where faster (default), 2 = always
     kEcPersistent,   // BLBRS_EC_PERSISTENT: fused encode+CRC on the persistent segment kernel, the fallback
                      // for shapes the tile-grid kernel does not take (0; 1 forces it where it applies)
-    kRtc,            // BLBRS_RTC: run-time decode networks 0 = off (default), 1 = compiled in the
-                     // background, 2 = compiled by the caller (rtc.hpp)
+    kRtc,            // BLBRS_RTC: run-time decode networks 0 = off, 1 = compiled in the
+                     // background (default since round 6), 2 = compiled by the caller (rtc.hpp)
     kRtcWide,        // BLBRS_RTC_WIDE: a decode pass takes a network when k + rows > this (13: RS(12,5)-wide
                      // passes, where the tables are VALU-bound; narrower ones measured +-1-3 %)
     kCount

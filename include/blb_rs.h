@@ -468,12 +468,14 @@ int blbrs_set_tuning(const char* name, long value);
 int blbrs_get_tuning(const char* name, long* value);
 
 /* Decode networks generated per erasure pattern and compiled with hipRTC.
- * Off by default (BLBRS_RTC = 0): the library does not link hipRTC and opens it (dlopen) only
- * when a network is first requested.  With BLBRS_RTC = 1 a wide decode pass
- * (k + rows > BLBRS_RTC_WIDE) requests its network on first use; it compiles in the background (a
- * host-only thread, no HIP call) and the pass runs the table kernel until the network is compiled;
- * the next launch of the pass then loads the code object in its own thread.  With BLBRS_RTC = 2
- * the first call compiles and loads it.  hipRTC missing = a compile failure: tables. */
+ * The library does not link hipRTC; it opens it (dlopen) when a network is first requested.
+ * With BLBRS_RTC = 1 (the default since round 6) a wide decode pass of at least 2 rows
+ * (k + rows > BLBRS_RTC_WIDE = 13: blb's RS(12,5) recovery RPC and multi-row ReconstructData)
+ * requests its network on first use; it compiles in the background (a host-only thread, no HIP
+ * call) and the pass runs the table kernel until the network is compiled; the next launch of the
+ * pass then loads the code object in its own thread.  With BLBRS_RTC = 2 the first call compiles
+ * and loads it; BLBRS_RTC = 0 keeps every pass on tables and hipRTC out of the process.  hipRTC
+ * missing = a compile failure: tables. */
 typedef struct {
     uint64_t requested;  /* networks requested (one per pass, mode, addressing, device) */
     uint64_t compiled;   /* distinct sources compiled */

@@ -127,10 +127,12 @@ def test_compiled_network_covers_blb_classes(knob):
     assert [nets[s]["code"] for s in ((12, 5), (10, 4), (8, 3), (6, 3), (3, 2))] == [True, True, True, False, False]
     assert [nets[s]["tile"] for s in ((12, 5), (10, 4), (8, 3), (6, 3))] == [True, True, False, False]
     assert [nets[s]["pack"] for s in ((12, 5), (10, 4), (8, 3), (6, 3))] == [True, True, True, False]
-    # run-time networks are off by default (BLBRS_RTC = 0); opted in, wide k outside the list takes one
-    assert nets[(14, 4)] == {"code": False, "tile": False, "pack": False, "rtc": False}
+    # run-time networks compile in the background by default (BLBRS_RTC = 1): wide k outside the
+    # compiled list takes one; BLBRS_RTC = 0 keeps it on tables
+    assert nets[(14, 4)] == {"code": False, "tile": False, "pack": False, "rtc": True}
+    knob("BLBRS_RTC", 0)
+    assert rs.New(14, 4).compiled_network() == {"code": False, "tile": False, "pack": False, "rtc": False}
     knob("BLBRS_RTC", 1)
-    assert rs.New(14, 4).compiled_network() == {"code": False, "tile": False, "pack": False, "rtc": True}
     assert not rs.New(12, 5).compiled_network()["rtc"]   # the compiled encode network wins
     knob("BLBRS_BITSLICE", 0)
     assert not any(rs.New(12, 5).compiled_network().values())

@@ -17,10 +17,11 @@ the same process:
   pack_encode_rs6_3_distinct  PackEncode of all B*k data pieces, distinct sources (pack_encode_kernel)
   pack_encode_rs8_3_distinct  the same at RS(8,3) B=512
   then RS(12,5) B=480 (the bench's recovery batch): EncodeBatch and EncodeBatchCRC(65532) on the
-  compiled network, a VerifyBatch, and blb's recovery shapes with the shipped default knobs
-  (the v_perm table kernel): the RPC with 1 and 5 bad data pieces (the first 12 good pieces
-  read, all 5 absent slots rebuilt) and the client's 5-row ReconstructData; then the same 1-bad
-  RPC on its opt-in run-time network (BLBRS_RTC = 2: compiled by the warm-up).
+  compiled network, a VerifyBatch, and blb's recovery shapes with the shipped default knobs (the
+  pass's run-time network, compiled in the background after a first call on tables): the RPC
+  with 1 and 5 bad data pieces (the first 12 good pieces read, all 5 absent slots rebuilt) and
+  the client's 5-row ReconstructData; then the same 1-bad RPC on the v_perm tables
+  (BLBRS_RTC = 0).
 
 Prints the op plan (label, kernel-name needle, launches) and the libblbrs.so sha256 as one
 JSON line; the summary consumes dispatches op by op in that order."""
@@ -156,12 +157,17 @@ rpc1, rpc5 = first_k_good(spread[:1]), first_k_good(spread)
 ok2 = bool(oks2[-1].all())
 for label, present, data_only, rows in (("rpc_1bad_rs12_5", rpc1, False, m2), ("rpc_5bad_rs12_5", rpc5, False, m2),
                                         ("client_rows5_rs12_5", rpc5, True, m2)):
+    # The shipped default (BLBRS_RTC = 1): the first call runs the tables and requests the pass's
+    # network, compiled in the background; once compiled the op's launches run the network.
+    check(f"request_network_{label}", "rs_code_kernel",
+          lambda p=present, d=data_only: enc2.ReconstructBatch(st, p, data_only=d))
+    rs.rtc_wait(120000)
     op(label, "rs_code_kernel", lambda p=present, d=data_only: enc2.ReconstructBatch(st, p, data_only=d),
-       B2 * (k2 + rows) * S, present=[i for i in range(n2) if present[i]], knobs="shipped default (tables)")
+       B2 * (k2 + rows) * S, present=[i for i in range(n2) if present[i]], knobs="shipped default (run-time network)")
     ok2 = ok2 and bool(check(f"verify_after_{label}", "rs_code_kernel", lambda: enc2.VerifyBatch(st)).all())
-with rs.tuning(BLBRS_RTC=2):
-    op("rpc_1bad_rs12_5_rtc_network", "rs_code_kernel", lambda: enc2.ReconstructBatch(st, rpc1), wb,
-       present=[i for i in range(n2) if rpc1[i]], knobs="BLBRS_RTC=2")
+with rs.tuning(BLBRS_RTC=0):
+    op("rpc_1bad_rs12_5_tables", "rs_code_kernel", lambda: enc2.ReconstructBatch(st, rpc1), wb,
+       present=[i for i in range(n2) if rpc1[i]], knobs="BLBRS_RTC=0")
 ok2 = ok2 and bool(enc2.VerifyBatch(st).all())
 lib = _lib.LIB_PATH
 print(json.dumps({"lib": lib, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
