@@ -171,9 +171,11 @@ def test_gpu_wrong_tag_dev_ptrs_recorded_per_device():
 @pytest.mark.gpu
 def test_gpu_default_recovery_compiles_its_network_in_the_background():
     """blb's widest recovery shape (RS(12,5), 5 bad pieces, every absent slot rebuilt) with
-    BLBRS_RTC = 0 runs on tables and never maps hipRTC; with the default knobs the first call
+    BLBRS_RTC = 0 runs on tables and requests no network; with the default knobs the first call
     runs on tables while its network compiles in the background, and once compiled (rtc_wait)
-    the pass loads and runs the network -- the same bytes every time."""
+    the pass loads and runs the network -- the same bytes every time.  (torch's ROCm build maps
+    its own libhiprtc, so this torch process cannot show the library leaving hipRTC unmapped:
+    test_library_does_not_link_hiprtc checks that without torch.)"""
     code = r'''
 import numpy as np, torch
 from blb_amd import reedsolomon as rs
@@ -194,15 +196,15 @@ def run():
     assert np.array_equal(to_numpy(st), host)
 rs.set_tuning("BLBRS_RTC", 0)
 run()
-assert rs.rtc_stats()["requested"] == 0
-print("MAPS1", "libhiprtc" in open("/proc/self/maps").read())
+assert rs.rtc_stats()["requested"] == 0 and rs.rtc_stats()["loaded"] == 0, rs.rtc_stats()
+print("TABLES OK")
 rs.set_tuning("BLBRS_RTC", 1)   # the default
 run()                            # tables; the network is requested and compiles in the background
 assert rs.rtc_stats()["requested"] >= 1, rs.rtc_stats()
 assert rs.rtc_wait(120000), rs.rtc_stats()
 run()                            # loads and runs the network
 assert rs.rtc_stats()["loaded"] >= 1 and rs.rtc_stats()["failed"] == 0, rs.rtc_stats()
-print("MAPS2", "libhiprtc" in open("/proc/self/maps").read())
+print("NETWORK OK", rs.rtc_stats())
 '''
     out = _maps_after(code, torch_first=True)
-    assert "MAPS1 False" in out and "MAPS2 True" in out, out[-2000:]
+    assert "TABLES OK" in out and "NETWORK OK" in out, out[-2000:]
