@@ -43,6 +43,13 @@ def test_new_on_argument_checks():
     assert lib.blbrs_buffer_get(1, None, None) == rs.ErrInvalidArgument.code
 
 
+def test_host_batch_rejects_negative_nstreams():
+    """blbrs_encode_host_batch: nstreams < 0 is INVALID_ARG, checked before anything else."""
+    enc = rs.New(6, 3)
+    with pytest.raises(rs.ErrInvalidArgument):
+        enc.EncodeHostBatch([[np.zeros(64, np.uint8) for _ in range(9)]], nstreams=-1)
+
+
 def test_device_calls_fail_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
@@ -103,10 +110,11 @@ def test_device_list_lanes_concurrent_host_calls(oracle_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pinned", [False, True])
-def test_device_list_host_batch_split(oracle_lib, pinned):
+@pytest.mark.parametrize("pinned,nstreams", [(False, 0), (True, 0), (True, 3), (False, 3)])
+def test_device_list_host_batch_split(oracle_lib, pinned, nstreams):
     """EncodeHostBatch splits its stripes contiguously over [0, 0] (two host threads, two
-    workers); pageable stripes go through the staging ring, pinned ones zero-copy."""
+    workers); pageable stripes go through the staging ring, pinned ones zero-copy -- or, with
+    nstreams >= 1, through the copy engines, both parts' rings on the one device at once."""
     import torch
     k, m, B, S = 10, 4, 7, 3 * MIB + 4100
     enc = rs.New(k, m, devices=[0, 0])
@@ -118,7 +126,7 @@ def test_device_list_host_batch_split(oracle_lib, pinned):
     host[:, :k] = rng.integers(0, 256, (B, k, S), dtype=np.uint8)
     host[:, k:] = 0xC3
     stripes = [[host[b, i] for i in range(k + m)] for b in range(B)]
-    enc.EncodeHostBatch(stripes)
+    enc.EncodeHostBatch(stripes, nstreams=nstreams)
     for b in range(B):
         ref = _oracle_parity(oracle_lib, k, m, [host[b, i] for i in range(k)])
         for j in range(m):
