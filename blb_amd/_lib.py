@@ -94,7 +94,8 @@ SIGNATURES = {
 class DeviceStats(ctypes.Structure):
     """blbrs_device_stats"""
     _fields_ = [("workers", ctypes.c_uint64), ("idle", ctypes.c_uint64), ("waits", ctypes.c_uint64),
-                ("staging_bytes", ctypes.c_uint64), ("calls", ctypes.c_uint64), ("inflight", ctypes.c_int64)]
+                ("staging_bytes", ctypes.c_uint64), ("calls", ctypes.c_uint64), ("inflight", ctypes.c_int64),
+                ("done_waits", ctypes.c_uint64), ("done_fallbacks", ctypes.c_uint64)]
 
 
 class PoolStats(ctypes.Structure):

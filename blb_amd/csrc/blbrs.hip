@@ -380,6 +380,12 @@ struct Stripes {
     bool aligned = false;
     uint32_t tag = 0;                // the table's tag (rt::tag_entries)
     uint32_t* fault = nullptr;       //   and the record its launches report a wrong entry to
+    // A small host call (store passes only): every pass on rs_small_kernel, the last one
+    // publishing done_seq to done_word when that is set (rs_small.hpp).
+    bool small = false;
+    uint32_t* done_word = nullptr;
+    uint32_t* done_count = nullptr;
+    uint32_t done_seq = 0;
 };
 
 // Launch every pass of `plan` over `batch` stripes.
@@ -409,6 +415,12 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         if (st.ninline) {
             if (st.ninline > static_cast<uint32_t>(kInlinePtrs)) return fail(BLBRS_ERR_INVALID_ARG, "inline table too long");
             std::memcpy(a.inl, st.inl, st.ninline * sizeof(uint64_t));
+        }
+        if (st.small && mode == Mode::kStore) {
+            const bool last = &ps == &plan.passes.back();
+            const hipError_t e = launch_small(a, last ? st.done_word : nullptr, st.done_count, st.done_seq, stream);
+            if (e != hipSuccess) return hip_fail(e, "launch rs_small_kernel");
+            continue;
         }
         Mode m = mode;
         if (mode == Mode::kStoreVerify) {  // per pass: all stored, all compared, or mixed
@@ -511,6 +523,30 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         (void)hipStreamSynchronize(w->s[1]);
         return rc_;
     };
+    // A single-launch call (the two forms below, or one unit of the slot pipeline) runs on the
+    // small-call kernel and ends on its completion word when it is small and has no verify flag
+    // to copy back; otherwise on a stream wait.
+    size_t call_bytes = 0;
+    for (int i = 0; i < n; ++i) call_bytes += touched[i] ? batch * S : 0;
+    const bool use_done = !verify && call_bytes <= rt::kDoneMaxBytes && tune::get(tune::kDoneWord) != 0;
+    auto launch_steps = [&](const Stripes& st, size_t nb, size_t len, int* rc_out) {
+        uint32_t seq = 0;
+        if (use_done) {
+            if ((*rc_out = w->ensure_done())) return seq;
+            seq = w->next_done_seq();
+        }
+        for (size_t t = 0; t < steps.size(); ++t) {
+            Stripes x = st;
+            x.small = use_done;
+            if (use_done && t + 1 == steps.size()) {
+                x.done_word = w->done_dev;
+                x.done_count = w->done_count;
+                x.done_seq = seq;
+            }
+            if ((*rc_out = run_plan(*plans[t], x, nb, len, steps[t].mode, w->flag, w->s[0]))) return seq;
+        }
+        return seq;
+    };
     // Per-slot addressing: device shards and pinned host shards are used in place (pinned ones
     // read and written by the kernels over PCIe, both link directions busy at once); only
     // pageable shards are staged.  blb's degraded read has k pool buffers in and the user's
@@ -550,13 +586,17 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         hipError_t e = hipSuccess;
         if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
         if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
-        for (size_t t = 0; t < steps.size(); ++t)
-            if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
-        if (verify && (rc = w->ensure_bounce(0))) return drain(rc);  // the pinned flag word
-        if (verify) e = hipMemcpyAsync(w->flag_host, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
-        const hipError_t f = hipStreamSynchronize(w->s[0]);
-        if (e == hipSuccess) e = f;
-        if (e != hipSuccess) return drain(hip_fail(e, "zero-copy call"));
+        const uint32_t seq = launch_steps(st, batch, S, &rc);
+        if (rc) return drain(rc);
+        if (use_done) {
+            if ((rc = w->wait_done(seq))) return drain(rc);
+        } else {
+            if (verify && (rc = w->ensure_bounce(0))) return drain(rc);  // the pinned flag word
+            if (verify) e = hipMemcpyAsync(w->flag_host, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
+            const hipError_t f = hipStreamSynchronize(w->s[0]);
+            if (e == hipSuccess) e = f;
+            if (e != hipSuccess) return drain(hip_fail(e, "zero-copy call"));
+        }
         if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
         if (ok) *ok = verify && *w->flag_host ? 0 : 1;
         return BLBRS_OK;
@@ -609,12 +649,16 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         hipError_t e = hipSuccess;
         if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
         if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
-        for (size_t t = 0; t < steps.size(); ++t)
-            if ((rc = run_plan(*plans[t], st, batch, S, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
-        if (verify) e = hipMemcpyAsync(w->flag_host, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
-        const hipError_t f = hipStreamSynchronize(w->s[0]);
-        if (e == hipSuccess) e = f;
-        if (e != hipSuccess) return drain(hip_fail(e, "staged call"));
+        const uint32_t seq = launch_steps(st, batch, S, &rc);
+        if (rc) return drain(rc);
+        if (use_done) {
+            if ((rc = w->wait_done(seq))) return drain(rc);
+        } else {
+            if (verify) e = hipMemcpyAsync(w->flag_host, w->flag, sizeof(int32_t), hipMemcpyDeviceToHost, w->s[0]);
+            const hipError_t f = hipStreamSynchronize(w->s[0]);
+            if (e == hipSuccess) e = f;
+            if (e != hipSuccess) return drain(hip_fail(e, "staged call"));
+        }
         if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
         for (size_t b = 0; b < batch; ++b)
             for (int i = 0; i < n; ++i) {
@@ -652,6 +696,8 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     if ((rc = w->ensure_bounce(2 * slot_bytes))) return rc;
     if ((rc = w->ensure_events())) return rc;
     const size_t per_stripe = (S + chunk - 1) / chunk, units = batch * per_stripe;
+    const bool one_done = use_done && units == 1;
+    uint32_t done_seq = 0;
     hipError_t e = hipSuccess;
     if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
     if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
@@ -700,6 +746,11 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             st.inl = inl;
             st.ninline = static_cast<uint32_t>(n);
         }
+        if (one_done) {  // a single unit: the small call's kernel and its completion word
+            done_seq = launch_steps(st, 1, len, &rc);
+            if (rc) return drain(rc);
+            continue;
+        }
         for (size_t t = 0; t < steps.size(); ++t)
             if ((rc = run_plan(*plans[t], st, 1, len, steps[t].mode, w->flag, w->s[0]))) return drain(rc);
         if ((e = hipEventRecord(w->ev[sl], w->s[0])) != hipSuccess) return drain(hip_fail(e, "staged call"));
@@ -711,7 +762,11 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         if ((rc = rt::check_fault(w->fault, "host call"))) return drain(rc);
         copy_out(units - 2);
     }
-    if ((e = hipStreamSynchronize(w->s[0])) != hipSuccess) return drain(hip_fail(e, "staged call"));
+    if (one_done) {
+        if ((rc = w->wait_done(done_seq))) return drain(rc);
+    } else if ((e = hipStreamSynchronize(w->s[0])) != hipSuccess) {
+        return drain(hip_fail(e, "staged call"));
+    }
     if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
     copy_out(units - 1);
     if (ok) *ok = verify && *w->flag_host ? 0 : 1;

@@ -1,10 +1,12 @@
 // rs_kernels.hip -- launch policy and ahead-of-time instantiations of rs_code_kernel
-// (rs_code.hpp): the v_perm table path for every shape and the compiled encode networks.
+// (rs_code.hpp): the v_perm table path for every shape and the compiled encode networks; and
+// rs_small_kernel (rs_small.hpp), the latency kernel of small host calls.
 #include "rs_kernels.hpp"
 
 #include <algorithm>
 
 #include "rs_code.hpp"
+#include "rs_small.hpp"
 #include "rtc.hpp"
 #include "tuning.hpp"
 
@@ -143,6 +145,67 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc:
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+namespace {
+
+using SmallFn = void (*)(code::SmallArgs);
+
+template <int K>
+SmallFn small_rows(int rows) {
+    switch (rows) {
+        case 1: return code::rs_small_kernel<K, 1>;
+        case 2: return code::rs_small_kernel<K, 2>;
+        case 3: return code::rs_small_kernel<K, 3>;
+        case 4: return code::rs_small_kernel<K, 4>;
+        case 5: return code::rs_small_kernel<K, 5>;
+        default: break;
+    }
+    if constexpr (K == 0) {
+        switch (rows) {
+            case 6: return code::rs_small_kernel<0, 6>;
+            case 7: return code::rs_small_kernel<0, 7>;
+            case 8: return code::rs_small_kernel<0, 8>;
+            default: break;
+        }
+    }
+    return nullptr;
+}
+
+SmallFn pick_small(int k, int rows) {
+    if (rows <= kMaxTemplRows) {
+        switch (k) {
+#define BLBRS_CASE(KK) case KK: return small_rows<KK>(rows);
+            BLBRS_K_LIST(BLBRS_CASE)
+#undef BLBRS_CASE
+            default: break;
+        }
+    }
+    return small_rows<0>(rows);
+}
+
+}  // namespace
+
+hipError_t launch_small(const CodeArgs& args, uint32_t* done_word, uint32_t* done_count, uint32_t seq,
+                        hipStream_t stream) {
+    if (args.rows < 1 || args.rows > kMaxRows || args.k < 1 || args.base) return hipErrorInvalidValue;
+    if (done_word && (!done_count || seq == 0)) return hipErrorInvalidValue;
+    if (!args.ptrs && static_cast<uint64_t>(args.B) * args.nshards > kInlinePtrs) return hipErrorInvalidValue;
+    const uint64_t chunks = (args.S + kTileBytes - 1) / kTileBytes;
+    const uint64_t total = static_cast<uint64_t>(args.B) * chunks;
+    if (args.B == 0 || args.S == 0 || total > 0x7FFFFFFFull) return hipErrorInvalidValue;  // callers: small calls
+    const SmallFn fn = pick_small(args.k, args.rows);
+    if (!fn) return hipErrorInvalidValue;
+    code::SmallArgs s{};
+    s.c = args;
+    s.c.tiles_per_stripe = static_cast<uint32_t>(chunks);
+    s.c.xcd_remap = 0;
+    s.done_word = done_word;
+    s.done_count = done_count;
+    s.done_seq = seq;
+    const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(total, 4096));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, s);
+    return hipGetLastError();
 }
 
 const char* kernel_name(int k, int rows, Mode mode, bool parity) {

@@ -77,6 +77,11 @@ hipError_t launch_code(const CodeArgs& args, Mode mode, hipStream_t stream, rtc:
 
 // Name of the kernel instantiation launch_code() would pick (for profiling/tests).
 const char* kernel_name(int k, int rows, Mode mode, bool parity = false);
+// A store pass of a small host call on rs_small_kernel (rs_small.hpp): one workgroup per 4 KiB
+// column chunk of each stripe, pointer-table addressing.  With done_word set, the launch's last
+// workgroup publishes `seq` there (done_count: the device word counting workgroups, at 0).
+hipError_t launch_small(const CodeArgs& args, uint32_t* done_word, uint32_t* done_count, uint32_t seq,
+                        hipStream_t stream);
 #endif
 
 

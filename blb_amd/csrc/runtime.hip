@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <shared_mutex>
@@ -54,6 +55,7 @@ std::vector<int> g_defaults;   // empty = not chosen yet
 constexpr int kMaxDevices = 64;
 std::atomic<int64_t> g_load[kMaxDevices];
 std::atomic<uint64_t> g_stage_bytes[kMaxDevices];
+std::atomic<uint64_t> g_done_waits[kMaxDevices], g_done_fallbacks[kMaxDevices];
 
 void stage_add(int dev, int64_t delta) {
     if (dev >= 0 && dev < kMaxDevices) g_stage_bytes[dev].fetch_add(static_cast<uint64_t>(delta));
@@ -407,7 +409,11 @@ int Worker::ensure_bounce(size_t bytes) {
     if (!flag_host) BLBRS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&flag_host), 64, hipHostMallocDefault));
     if (bytes <= bounce_cap) return BLBRS_OK;
     note_released(bounce, bounce_cap, "worker staging (grown)");
-    if (bounce) (void)hipHostFree(bounce);  // every call that used it ended with a sync of its streams
+    if (bounce) {
+        // Calls that ended on a completion word leave their launch's tail on the streams.
+        for (auto& x : s) (void)hipStreamSynchronize(x);
+        (void)hipHostFree(bounce);
+    }
     stage_add(device, -static_cast<int64_t>(bounce_cap));
     bounce = nullptr;
     bounce_dev = 0;
@@ -430,8 +436,8 @@ int Worker::ensure_bounce(size_t bytes) {
 int Worker::upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned,
                          uint32_t* tag) {
     if (count > tab_cap) {
-        // The previous copy out of tab_host has completed: every call that used it ended with
-        // a sync of s[0].
+        // The previous copy out of tab_host completes before the tables are released.
+        for (auto& x : s) (void)hipStreamSynchronize(x);
         note_released(tab_host, tab_cap * 8, "worker table host (grown)");
         note_released(tab_dev, tab_cap * 8, "worker table device (grown)");
         if (tab_host) (void)hipHostFree(tab_host);
@@ -448,6 +454,59 @@ int Worker::upload_table(const uint64_t* ptrs, size_t count, const uint64_t** de
     if (int rc = tag_entries(ptrs, count, *tag, tab_host, aligned)) return rc;
     BLBRS_HIP_TRY(hipMemcpyAsync(tab_dev, tab_host, count * 8, hipMemcpyHostToDevice, s[0]));
     *dev_out = tab_dev;
+    return BLBRS_OK;
+}
+
+int Worker::ensure_done() {
+    if (done_host) return BLBRS_OK;
+    uint32_t* h = nullptr;
+    BLBRS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h), 64, hipHostMallocCoherent | hipHostMallocMapped));
+    *h = 0;
+    void* d = nullptr;
+    uint32_t* cnt = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+    if (e == hipSuccess && !d) e = hipErrorInvalidValue;
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&cnt), sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), s[0]);
+    if (e == hipSuccess) e = hipStreamSynchronize(s[0]);
+    if (e != hipSuccess) {
+        if (cnt) (void)hipFree(cnt);
+        (void)hipHostFree(h);
+        return hip_fail(e, "completion word");
+    }
+    done_host = h;
+    done_dev = static_cast<uint32_t*>(d);
+    done_count = cnt;
+    return BLBRS_OK;
+}
+
+uint32_t Worker::next_done_seq() {
+    const uint32_t cur = __atomic_load_n(done_host, __ATOMIC_ACQUIRE);
+    do ++done_seq;
+    while (done_seq == 0 || done_seq == cur);
+    return done_seq;
+}
+
+int Worker::wait_done(uint32_t seq) {
+    using Clock = std::chrono::steady_clock;
+    const auto limit = Clock::now() + std::chrono::microseconds(kDoneSpinUs);
+    for (uint32_t spins = 1;; ++spins) {
+        if (__atomic_load_n(done_host, __ATOMIC_ACQUIRE) == seq) {
+            if (device >= 0 && device < kMaxDevices) g_done_waits[device].fetch_add(1, std::memory_order_relaxed);
+            return BLBRS_OK;
+        }
+        if (spins % 64 == 0 && Clock::now() > limit) break;
+        __builtin_ia32_pause();
+    }
+    if (device >= 0 && device < kMaxDevices) g_done_fallbacks[device].fetch_add(1, std::memory_order_relaxed);
+    hipError_t e = hipStreamSynchronize(s[0]);
+    if (e != hipSuccess) return hip_fail(e, "small call");
+    if (__atomic_load_n(done_host, __ATOMIC_ACQUIRE) != seq) {
+        // The launches finished without publishing (none carried the word): restart the count.
+        e = hipMemsetAsync(done_count, 0, sizeof(uint32_t), s[0]);
+        if (e == hipSuccess) e = hipStreamSynchronize(s[0]);
+        if (e != hipSuccess) return hip_fail(e, "completion word reset");
+    }
     return BLBRS_OK;
 }
 
@@ -468,6 +527,9 @@ void Worker::destroy() {
     if (fault) (void)hipHostFree(fault);
     if (bounce) (void)hipHostFree(bounce);
     if (flag_host) (void)hipHostFree(flag_host);
+    if (done_host) (void)hipHostFree(done_host);
+    if (done_count) (void)hipFree(done_count);
+    done_host = done_dev = done_count = nullptr;
     for (auto& e : ev)
         if (e) (void)hipEventDestroy(e);
     stage_add(device, -static_cast<int64_t>(bounce_cap));
@@ -593,6 +655,9 @@ int device_stats(int dev, blbrs_device_stats* out) {
     out->staging_bytes = dev >= 0 && dev < kMaxDevices ? g_stage_bytes[dev].load() : 0;
     out->calls = p.calls.load();
     out->inflight = load_of(dev);
+    const bool in = dev >= 0 && dev < kMaxDevices;
+    out->done_waits = in ? g_done_waits[dev].load(std::memory_order_relaxed) : 0;
+    out->done_fallbacks = in ? g_done_fallbacks[dev].load(std::memory_order_relaxed) : 0;
     return BLBRS_OK;
 }
 

@@ -145,6 +145,13 @@ constexpr size_t kBounceMaxBytes = size_t{512} << 10;
 // pinned staging, each at most this big: the CPU fills one slot while the kernel works in the
 // other.  Pageable memory is never handed to HIP's copy engines.
 constexpr size_t kPinnedSlotBytes = size_t{8} << 20;
+// Single-launch host calls touching at most this many shard bytes, with no verify flag to read
+// back, run on rs_small_kernel and end on its completion word (rs_small.hpp; BLBRS_DONE_WORD,
+// default on): the word arrives ~3 us before the stream's completion signal would wake the
+// caller (tools/sync_probe.hip).  The spin bound covers such a kernel many times
+// over; past it the thread waits for the stream.
+constexpr size_t kDoneMaxBytes = size_t{2} << 20;
+constexpr int kDoneSpinUs = 2000;
 
 struct Worker {
     int device = -1;
@@ -159,8 +166,22 @@ struct Worker {
     size_t bounce_cap = 0;
     int32_t* flag_host = nullptr;   // pinned landing word of the verify flag
     hipEvent_t ev[2] = {nullptr, nullptr};  // staging slot reuse (created on first use)
+    // Completion word of small calls (rs_small.hpp SmallArgs, created on first use): a coherent
+    // pinned word the call's last launch publishes its sequence number to, its device view, and
+    // the device-memory count of finished workgroups behind it.
+    uint32_t* done_host = nullptr;
+    uint32_t* done_dev = nullptr;
+    uint32_t* done_count = nullptr;
+    uint32_t done_seq = 0;
     int ensure_bounce(size_t bytes);
     int ensure_events();
+    int ensure_done();
+    // The next sequence number (never 0, never the word's current value).
+    uint32_t next_done_seq();
+    // Ends a call whose last launch on s[0] carries word `seq`: spins on the word for up to
+    // kDoneSpinUs, then waits for s[0] instead (which reports a fault; a finished launch that
+    // never published -- none was made -- restarts the count).  Counted per device.
+    int wait_done(uint32_t seq);
     // Copies `count` device addresses, tagged (*tag), to the worker's device table on stream s[0].
     int upload_table(const uint64_t* ptrs, size_t count, const uint64_t** dev_out, bool* aligned, uint32_t* tag);
     void destroy();

@@ -17,7 +17,7 @@ struct Def {
 };
 // Order = enum Knob.
 constexpr Def kDefs[kCount] = {
-    {"BLBRS_BITSLICE", 1}, {"BLBRS_EC_PERSISTENT", 0}, {"BLBRS_RTC", 1}, {"BLBRS_RTC_WIDE", 13},
+    {"BLBRS_BITSLICE", 1}, {"BLBRS_EC_PERSISTENT", 0}, {"BLBRS_RTC", 1}, {"BLBRS_RTC_WIDE", 13}, {"BLBRS_DONE_WORD", 1},
 };
 
 // The environment is read once, here (thread-safe static initialisation).

@@ -21,6 +21,8 @@ enum Knob : int {
                      // background (default since round 6), 2 = compiled by the caller (rtc.hpp)
     kRtcWide,        // BLBRS_RTC_WIDE: a decode pass takes a network when k + rows > this (13: RS(12,5)-wide
                      // passes, where the tables are VALU-bound; narrower ones measured +-1-3 %)
+    kDoneWord,       // BLBRS_DONE_WORD: small single-launch host calls end on their kernel's completion
+                     // word (1, default since round 6) or on a stream wait (0); runtime.hpp kDoneMaxBytes
     kCount
 };
 

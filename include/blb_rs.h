@@ -68,6 +68,9 @@ typedef struct {
     uint64_t staging_bytes;  /* pinned staging memory held by the device's workers */
     uint64_t calls;          /* host-memory calls and host-batch parts run on the device */
     int64_t inflight;        /* of which running now */
+    uint64_t done_waits;     /* small calls that ended on their kernel's completion word */
+    uint64_t done_fallbacks; /* small calls whose word did not come within the spin bound:
+                                they waited for the stream instead (which reports a fault) */
 } blbrs_device_stats;
 
 /* Pinned buffer pool counters (blbrs_get_pool_stats). */

@@ -32,6 +32,49 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(declared)
 
 
+_C_SIZES = {"uint64_t": 8, "int64_t": 8, "size_t": 8, "double": 8, "uint32_t": 4, "int32_t": 4, "int": 4}
+
+
+def header_structs():
+    """{typedef name: [(field, C type), ...]} of every plain typedef struct in the header."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for body, name in re.findall(r"typedef struct\s*\{(.*?)\}\s*(\w+)\s*;", text, flags=re.S):
+        fields = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            m = re.match(r"((?:const\s+)?\w+\s*\**)\s*(.*)", decl)
+            ctype, names = m.group(1).strip(), m.group(2)
+            for nm in names.split(","):
+                nm = nm.strip()
+                ptr = nm.startswith("*") or ctype.endswith("*")
+                fields.append((nm.lstrip("*").strip(), "ptr" if ptr else ctype))
+        out[name] = fields
+    return out
+
+
+def test_ctypes_structs_match_header():
+    """Every ctypes mirror of a header struct (blb_amd/_lib.py) has the header's fields, in its
+    order, and its size: a field added to the C side and not to the mirror would make every
+    counter after it read the wrong bytes."""
+    from blb_amd import _lib
+    structs = header_structs()
+    mirrors = [c for c in vars(_lib).values()
+               if isinstance(c, type) and issubclass(c, ctypes.Structure) and (c.__doc__ or "").startswith("blbrs_")]
+    assert len(mirrors) >= 6
+    for cls in mirrors:
+        fields = structs[cls.__doc__.strip()]
+        assert [f for f, _ in cls._fields_] == [f for f, _ in fields], cls.__doc__
+        size = 0
+        for _, t in fields:
+            w = 8 if t == "ptr" else _C_SIZES[t]
+            size = (size + w - 1) // w * w + w
+        size = (size + 7) // 8 * 8 if any(t == "ptr" or _C_SIZES.get(t) == 8 for _, t in fields) else size
+        assert ctypes.sizeof(cls) == size, (cls.__doc__, ctypes.sizeof(cls), size)
+
+
 def test_error_codes_match_header():
     from blb_amd import reedsolomon as rs
     text = open(HEADER).read()

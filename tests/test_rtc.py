@@ -114,7 +114,7 @@ def test_network_kernel_compiles_for_gfx950():
 
 
 def test_knobs_read_once_and_settable(knob):
-    for name in ("BLBRS_BITSLICE", "BLBRS_RTC", "BLBRS_RTC_WIDE", "BLBRS_EC_PERSISTENT"):
+    for name in ("BLBRS_BITSLICE", "BLBRS_RTC", "BLBRS_RTC_WIDE", "BLBRS_EC_PERSISTENT", "BLBRS_DONE_WORD"):
         v = rs.get_tuning(name)
         knob(name, v + 1)
         assert rs.get_tuning(name) == v + 1

@@ -328,3 +328,66 @@ def test_gpu_per_read_new_builds_each_plan_once():
         if i == 0:
             before = rs.plan_stats()
     assert rs.plan_stats() == before, (before, rs.plan_stats())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m", [(6, 3), (10, 3), (12, 5)])
+def test_gpu_small_calls_end_on_completion_word(knob, k, m):
+    """Small single-launch host calls with no verify flag run on rs_small_kernel and end on its
+    completion word (rs_small.hpp, runtime.hpp kDoneMaxBytes): Encode, ReconstructData and
+    Reconstruct of pageable (staged) and pool (in place) shards, whole 4 KiB chunks and ragged
+    ends, are bit-exact against the restatement; each call counts one done wait and none falls
+    back to the stream wait.  Verify, and BLBRS_DONE_WORD = 0, wait for the stream and count
+    nothing.  RS(10,3) / RS(12,5) take the kernel's 16-input load group."""
+    knob("BLBRS_DONE_WORD", 1)
+    rng = np.random.default_rng(k * 100 + m)
+    before = rs.device_stats(0)
+    calls = 0
+    for S in (4096, 12000, 65536, 98765):
+        data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+        full = data + list(N.encode(k, m, data))
+        for pooled in (False, True):
+            bufs = []
+
+            def shard(src):
+                if not pooled:
+                    return src.copy()
+                b = rs.GetBuffer(S)
+                b[:] = src
+                bufs.append(b)
+                return b
+            try:
+                enc = rs.New(k, m)
+                sh = [shard(full[j]) for j in range(k)] + [shard(np.full(S, 0xEE, np.uint8)) for _ in range(m)]
+                enc.Encode(sh)
+                for j in range(k, k + m):
+                    assert np.array_equal(sh[j], full[j]), (S, pooled, "encode", j)
+                sh = [shard(full[j]) for j in range(k + m)]
+                sh[1] = None
+                sh[k + m - 1] = None
+                enc.ReconstructData(sh)
+                assert np.array_equal(sh[1], full[1]), (S, pooled, "reconstruct data")
+                sh = [shard(full[j]) for j in range(k + m)]
+                sh[0] = None
+                sh[k] = None
+                enc.Reconstruct(sh)
+                assert np.array_equal(sh[0], full[0]) and np.array_equal(sh[k], full[k]), (S, pooled, "reconstruct")
+                calls += 3
+            finally:
+                for b in bufs:
+                    rs.PutBuffer(b)
+    mid = rs.device_stats(0)
+    assert mid["done_fallbacks"] == before["done_fallbacks"]
+    assert mid["done_waits"] - before["done_waits"] == calls, (before, mid, calls)
+    enc = rs.New(k, m)
+    S = 4096
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+    full = data + list(N.encode(k, m, data))
+    assert enc.Verify([f.copy() for f in full])
+    knob("BLBRS_DONE_WORD", 0)
+    sh = [f.copy() for f in full]
+    sh[2] = None
+    enc.ReconstructData(sh)
+    assert np.array_equal(sh[2], full[2])
+    after = rs.device_stats(0)
+    assert after["done_waits"] == mid["done_waits"] and after["done_fallbacks"] == mid["done_fallbacks"]
