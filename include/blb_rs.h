@@ -24,7 +24,9 @@
  *     caller's buffer), or NULL for a parity slot that ReconstructData will not produce.
  *   - Outputs are fully overwritten, never accumulated into (rpc.GetBuffer returns
  *     un-zeroed pooled buffers, pkg/rpc/pool.go:28-43).
- *   - No pointer is retained after a call returns (cgo rule).
+ *   - No pointer is retained after a call returns (cgo rule).  A small host call may return
+ *     on its kernel's completion word, before the dispatch has retired: the word is published
+ *     after every output is written, and the kernel touches no caller memory after it.
  *   - All functions are thread-safe and none changes the calling thread's current HIP
  *     device.  Host-memory calls run on the least-loaded device of the encoder's device
  *     list (blbrs_new_on; blbrs_new takes the process default list), each on a stream worker
@@ -464,7 +466,7 @@ int blbrs_lane_policy(const int* nodes, const int64_t* loads, size_t n, size_t s
 /* ---- A/B knobs and run-time networks ---- */
 
 /* The library's tuning knobs (BLBRS_BITSLICE, BLBRS_EC_PERSISTENT, BLBRS_RTC,
- * BLBRS_RTC_WIDE; blb_amd/csrc/tuning.hpp), each a choice between shipped policies,
+ * BLBRS_RTC_WIDE, BLBRS_DONE_WORD; blb_amd/csrc/tuning.hpp), each a choice between shipped policies,
  * start from the environment, read once, and change only here -- never by setenv while the
  * library runs.  INVALID_ARG for an unknown name. */
 int blbrs_set_tuning(const char* name, long value);
