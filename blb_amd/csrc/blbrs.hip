@@ -102,6 +102,7 @@ struct DevPass {
     const int32_t* in_idx = nullptr;
     const int32_t* out_idx = nullptr;
     const uint32_t* tables = nullptr;
+    std::vector<int32_t> in_idx_h, out_idx_h;  // host copies (one-stripe small calls resolve entries)
     int k_in = 0, rows = 0;
     int nstore = -1;
     bool parity = false;
@@ -133,6 +134,8 @@ int upload(const HostPlan& hp, int device, std::unique_ptr<DevPlan>& out) {
         d.nstore = ps.nstore;
         d.parity = ps.parity;
         d.coef = ps.coef;
+        d.in_idx_h = ps.in_idx;
+        d.out_idx_h = ps.out_idx;
         d.net = std::make_shared<rtc::NetSlot>();
         const size_t n_in = ps.in_idx.size() * 4, n_out = round_up(ps.out_idx.size() * 4, 16);
         const size_t off_out = round_up(n_in, 16), off_tab = off_out + n_out;
@@ -418,7 +421,13 @@ int run_plan(const DevPlan& plan, const Stripes& st, size_t batch, size_t S, Mod
         }
         if (st.small && mode == Mode::kStore) {
             const bool last = &ps == &plan.passes.back();
-            const hipError_t e = launch_small(a, last ? st.done_word : nullptr, st.done_count, st.done_seq, stream);
+            uint32_t* word = last ? st.done_word : nullptr;
+            // One stripe with an inline table: the kernel gets the pass's entries resolved.
+            hipError_t e = batch == 1 && st.ninline
+                               ? launch_small1(a, ps.in_idx_h.data(), ps.out_idx_h.data(), word, st.done_count,
+                                               st.done_seq, stream)
+                               : hipErrorNotSupported;
+            if (e == hipErrorNotSupported) e = launch_small(a, word, st.done_count, st.done_seq, stream);
             if (e != hipSuccess) return hip_fail(e, "launch rs_small_kernel");
             continue;
         }

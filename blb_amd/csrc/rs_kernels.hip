@@ -208,6 +208,71 @@ hipError_t launch_small(const CodeArgs& args, uint32_t* done_word, uint32_t* don
     return hipGetLastError();
 }
 
+namespace {
+
+using Small1Fn = void (*)(code::Small1Args);
+
+template <int K>
+Small1Fn small1_rows(int rows) {
+    switch (rows) {
+        case 1: return code::rs_small1_kernel<K, 1>;
+        case 2: return code::rs_small1_kernel<K, 2>;
+        case 3: return code::rs_small1_kernel<K, 3>;
+        case 4: return code::rs_small1_kernel<K, 4>;
+        case 5: return code::rs_small1_kernel<K, 5>;
+        default: return nullptr;
+    }
+}
+
+Small1Fn pick_small1(int k, int rows) {
+    switch (k) {
+#define BLBRS_CASE(KK) case KK: return small1_rows<KK>(rows);
+        BLBRS_K_LIST(BLBRS_CASE)
+#undef BLBRS_CASE
+        default: return nullptr;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_small1(const CodeArgs& args, const int32_t* in_idx, const int32_t* out_idx, uint32_t* done_word,
+                         uint32_t* done_count, uint32_t seq, hipStream_t stream) {
+    if (args.B != 1 || args.base || args.ptrs || !in_idx || !out_idx) return hipErrorNotSupported;
+    if (args.k > code::kSmall1MaxIn || args.rows < 1 || args.rows > kMaxRows) return hipErrorNotSupported;
+    const Small1Fn fn = pick_small1(args.k, args.rows);
+    if (!fn) return hipErrorNotSupported;
+    if (done_word && (!done_count || seq == 0)) return hipErrorInvalidValue;
+    if (args.S == 0) return hipErrorInvalidValue;
+    code::Small1Args s{};
+    s.tables = args.tables;
+    s.S = args.S;
+    s.fault = args.fault;
+    s.done_word = done_word;
+    s.done_count = done_count;
+    s.done_seq = seq;
+    s.ptr_tag = args.ptr_tag;
+    const uint64_t chunks = (args.S + kTileBytes - 1) / kTileBytes;
+    if (chunks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    s.chunks = static_cast<uint32_t>(chunks);
+    s.rows = args.rows;
+    s.aligned = args.aligned;
+    for (int j = 0; j < args.k; ++j) {
+        if (in_idx[j] < 0 || static_cast<uint32_t>(in_idx[j]) >= args.nshards || in_idx[j] >= kInlinePtrs)
+            return hipErrorInvalidValue;
+        s.in_e[j] = args.inl[in_idx[j]];
+        s.in_slot[j] = static_cast<uint8_t>(in_idx[j]);
+    }
+    for (int r = 0; r < args.rows; ++r) {
+        if (out_idx[r] < 0 || static_cast<uint32_t>(out_idx[r]) >= args.nshards || out_idx[r] >= kInlinePtrs)
+            return hipErrorInvalidValue;
+        s.out_e[r] = args.inl[out_idx[r]];
+        s.out_slot[r] = static_cast<uint8_t>(out_idx[r]);
+    }
+    const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(chunks, 4096));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kThreads), 0, stream, s);
+    return hipGetLastError();
+}
+
 const char* kernel_name(int k, int rows, Mode mode, bool parity) {
     const Choice ch = pick(k, rows, mode, true, bs::use(parity, k, rows, bs::kWideCode));
     return ch.cm      ? "rs_code_kernel<K,MR,MODE,ADDR,U,NT,true>"

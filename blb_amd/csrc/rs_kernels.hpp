@@ -82,6 +82,12 @@ const char* kernel_name(int k, int rows, Mode mode, bool parity = false);
 // workgroup publishes `seq` there (done_count: the device word counting workgroups, at 0).
 hipError_t launch_small(const CodeArgs& args, uint32_t* done_word, uint32_t* done_count, uint32_t seq,
                         hipStream_t stream);
+// The same for ONE stripe with an inline table (args.inl): the kernel (rs_small1_kernel) gets
+// the pass's tagged entries in plan order (in_idx / out_idx: the pass's host index lists), so
+// it loads no index or table entry itself.  hipErrorNotSupported for shapes it has no kernel for
+// (k outside the compiled list, more than 5 rows): the caller uses launch_small.
+hipError_t launch_small1(const CodeArgs& args, const int32_t* in_idx, const int32_t* out_idx, uint32_t* done_word,
+                         uint32_t* done_count, uint32_t seq, hipStream_t stream);
 #endif
 
 

@@ -15,8 +15,10 @@
 //    thread spins on that word instead of waiting for the stream's completion signal
 //    (tools/sync_probe.hip: 14.1 -> 10.9 us per 4 KiB call).
 // Store mode only (the calls that use it copy no verify flag back), pointer-table addressing
-// (host calls), the v_perm table multiply of rs_code.hpp.  The HBM kernels are not touched:
-// rs_code_kernel's code is unchanged by this header.
+// (host calls), the v_perm table multiply of rs_code.hpp.  A call of one stripe with an inline
+// table -- blb's degraded read -- takes rs_small1_kernel (below), which also drops the chain of
+// dependent index and table-entry loads.  The HBM kernels are not touched: rs_code_kernel's code
+// is unchanged by this header.
 #pragma once
 #include "rs_code.hpp"
 
@@ -77,14 +79,14 @@ __device__ __forceinline__ void code_chunk_vec16(const CodeArgs& a, uint32_t b, 
 // counts itself finished; the last one resets the count and publishes the sequence number with a
 // system-scope release.  A workgroup that faults never counts, so the host's bounded spin ends
 // in the stream wait that reports the fault.
-__device__ __forceinline__ void signal_done(const SmallArgs& s) {
+__device__ __forceinline__ void signal_done(uint32_t* word, uint32_t* count, uint32_t seq) {
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t before = __hip_atomic_fetch_add(s.done_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t before = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (before == gridDim.x - 1) {
-            __hip_atomic_store(s.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(s.done_word, s.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -113,7 +115,112 @@ __global__ __launch_bounds__(kThreads) void rs_small_kernel(SmallArgs s) {
             code_tile_slow<MR, 0, 1, 1>(a, b, chunk0);  // ragged end or unaligned shards: bytes
         }
     }
-    if (s.done_word) signal_done(s);
+    if (s.done_word) signal_done(s.done_word, s.done_count, s.done_seq);
+}
+
+// ---- one stripe, entries resolved by the host ----
+//
+// rs_small_kernel (and rs_code_kernel's partial tiles) find a shard's address through two
+// dependent scalar loads -- the plan's index, then the table entry at that index -- and the
+// table check walks every entry the same way before the first data load: ~30 serialized scalar
+// round trips for an RS(6,3) decode (the 4 KiB kernel took 8.7 us against 3.8 for the same PCIe
+// reads in tools/sync_probe.hip).  A one-stripe call with an inline table (blb's degraded read,
+// a single increment) needs none of that: the host hands the kernel the pass's tagged entries
+// in plan order, so the tag check and every address come from constant-offset loads of the
+// kernel arguments, the coefficient tables from constant offsets of one pointer, and every input
+// load issues before the first wait.
+constexpr int kSmall1MaxIn = 16;
+
+struct Small1Args {
+    const uint32_t* tables;         // device: [rows][k][5] v_perm words (the pass's plan)
+    uint64_t S;                     // shard bytes
+    uint32_t* fault;                // host-mapped table-check record (rs_code.hpp stripe_table_ok's format)
+    uint32_t* done_word;            // completion word, or null (a pass before the last)
+    uint32_t* done_count;
+    uint32_t done_seq;
+    uint32_t ptr_tag;
+    uint32_t chunks;                // 4 KiB column chunks
+    int32_t rows;                   // <= MR
+    int32_t aligned;                // every entry 16-byte aligned
+    uint64_t in_e[kSmall1MaxIn];    // tagged entries of the inputs, in plan order
+    uint64_t out_e[kMaxRows];       // and of the outputs
+    uint8_t in_slot[kSmall1MaxIn];  // their slots in the stripe (fault reports)
+    uint8_t out_slot[kMaxRows];
+};
+
+__device__ __forceinline__ uint8_t* entry_ptr(uint64_t e) { return reinterpret_cast<uint8_t*>(e & kPtrMask); }
+
+// Inputs [J0, J1) of a K-input pass into acc: unrolled over a range of at most 8 inputs so that
+// the body stays under the unroller's limit.
+template <int K, int MR, int J0, int J1, int NV>
+__device__ __forceinline__ void madd_range(const Small1Args& s, const V4 (&x)[K], uint32_t (&acc)[MR][NV]) {
+#pragma unroll
+    for (int j = J0; j < J1; ++j) {
+        uint32_t w[4];
+        unpack(x[j], w);
+        madd<MR, 4>(Groups<4>(w), [&](int r) { return as_const(s.tables) + (r * K + j) * 5; }, acc, s.rows);
+    }
+}
+
+template <int K, int MR>
+__global__ __launch_bounds__(kThreads) void rs_small1_kernel(Small1Args s) {
+    static_assert(K > 0 && K <= kSmall1MaxIn && MR <= kMaxRows, "shape");
+    int bad = -1;  // the first entry with a wrong tag: input j, or K + output r
+#pragma unroll
+    for (int j = K - 1; j >= 0; --j)
+        if (static_cast<uint32_t>(s.in_e[j] >> kPtrTagShift) != s.ptr_tag) bad = j;
+    if (bad < 0) {
+#pragma unroll
+        for (int r = MR - 1; r >= 0; --r)
+            if (r < s.rows && static_cast<uint32_t>(s.out_e[r] >> kPtrTagShift) != s.ptr_tag) bad = K + r;
+    }
+    if (bad >= 0) {  // nothing is dereferenced; the host fails the call naming the slot
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const uint64_t e = bad < K ? s.in_e[bad] : s.out_e[bad - K];
+            s.fault[1] = 0u;
+            s.fault[2] = bad < K ? s.in_slot[bad] : s.out_slot[bad - K];
+            s.fault[3] = s.ptr_tag;
+            s.fault[4] = static_cast<uint32_t>(e);
+            s.fault[5] = static_cast<uint32_t>(e >> 32);
+            __threadfence_system();
+            s.fault[0] = 1u;
+        }
+    } else {
+        for (uint32_t t = blockIdx.x; t < s.chunks; t += gridDim.x) {
+            const uint64_t chunk0 = static_cast<uint64_t>(t) * kTileBytes;
+            const uint64_t off = chunk0 + static_cast<uint64_t>(threadIdx.x) * kBytesPerThread;
+            V4 x[K];
+            uint32_t acc[MR][4] = {};
+            if (s.aligned && chunk0 + kTileBytes <= s.S) {  // uniform: every lane holds a whole 16 B
+#pragma unroll
+                for (int j = 0; j < K; ++j) x[j] = ld16<0>(entry_ptr(s.in_e[j]) + off);
+                __builtin_amdgcn_sched_barrier(0);
+                madd_range<K, MR, 0, (K < 8 ? K : 8), 4>(s, x, acc);
+                if constexpr (K > 8) madd_range<K, MR, 8, K, 4>(s, x, acc);
+#pragma unroll
+                for (int r = 0; r < MR; ++r)
+                    if (r < s.rows) st16<0>(entry_ptr(s.out_e[r]) + off, pack(acc[r]));
+            } else if (off < s.S) {  // the ragged end, or unaligned shards: per lane
+                const uint32_t nb = static_cast<uint32_t>(s.S - off < 16 ? s.S - off : 16);
+                const bool vec = s.aligned && nb == 16;
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const uint8_t* p = entry_ptr(s.in_e[j]) + off;
+                    x[j] = vec ? ld16<0>(p) : load_bytes(p, nb);
+                }
+                madd_range<K, MR, 0, (K < 8 ? K : 8), 4>(s, x, acc);
+                if constexpr (K > 8) madd_range<K, MR, 8, K, 4>(s, x, acc);
+#pragma unroll
+                for (int r = 0; r < MR; ++r) {
+                    if (r >= s.rows) break;
+                    uint8_t* q = entry_ptr(s.out_e[r]) + off;
+                    if (vec) st16<0>(q, pack(acc[r]));
+                    else store_bytes(q, pack(acc[r]), nb);
+                }
+            }
+        }
+    }
+    if (s.done_word) signal_done(s.done_word, s.done_count, s.done_seq);
 }
 
 }  // namespace code

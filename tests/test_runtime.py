@@ -338,7 +338,9 @@ def test_gpu_small_calls_end_on_completion_word(knob, k, m):
     Reconstruct of pageable (staged) and pool (in place) shards, whole 4 KiB chunks and ragged
     ends, are bit-exact against the restatement; each call counts one done wait and none falls
     back to the stream wait.  Verify, and BLBRS_DONE_WORD = 0, wait for the stream and count
-    nothing.  RS(10,3) / RS(12,5) take the kernel's 16-input load group."""
+    nothing.  One-stripe calls take rs_small1_kernel (entries resolved by the host), a host batch
+    of three stripes the multi-stripe rs_small_kernel, whose RS(10,3) / RS(12,5) load 16 inputs
+    as one group."""
     knob("BLBRS_DONE_WORD", 1)
     rng = np.random.default_rng(k * 100 + m)
     before = rs.device_stats(0)
@@ -376,6 +378,18 @@ def test_gpu_small_calls_end_on_completion_word(knob, k, m):
             finally:
                 for b in bufs:
                     rs.PutBuffer(b)
+    # Several stripes in one small call (a host batch that fits the worker's bounce buffer,
+    # runtime.hpp kBounceMaxBytes): the multi-stripe form of the kernel, whole chunk and ragged.
+    for S in (4096, 4000):
+        host = np.zeros((3, k + m, S), np.uint8)
+        host[:, :k] = rng.integers(0, 256, (3, k, S), dtype=np.uint8)
+        host[:, k:] = 0xEE
+        rs.New(k, m).EncodeHostBatch([[host[b, i] for i in range(k + m)] for b in range(3)])
+        for b in range(3):
+            ref = N.encode(k, m, [host[b, i] for i in range(k)])
+            for j in range(m):
+                assert np.array_equal(host[b, k + j], ref[j]), (S, "host batch", b, j)
+        calls += 1
     mid = rs.device_stats(0)
     assert mid["done_fallbacks"] == before["done_fallbacks"]
     assert mid["done_waits"] - before["done_waits"] == calls, (before, mid, calls)
