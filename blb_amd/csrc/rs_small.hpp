@@ -77,12 +77,14 @@ __device__ __forceinline__ void code_chunk_vec16(const CodeArgs& a, uint32_t b, 
 
 // Each workgroup makes its stores (outputs and the table-check record) visible to the host, then
 // counts itself finished; the last one resets the count and publishes the sequence number with a
-// system-scope release.  A workgroup that faults never counts, so the host's bounded spin ends
+// system-scope release (a grid of one publishes without counting).  A workgroup that faults never counts, so the host's bounded spin ends
 // in the stream wait that reports the fault.
 __device__ __forceinline__ void signal_done(uint32_t* word, uint32_t* count, uint32_t seq) {
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && gridDim.x == 1) {  // one workgroup (a 4 KiB piece): nothing to count
+        __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (threadIdx.x == 0) {
         const uint32_t before = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (before == gridDim.x - 1) {
             __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
