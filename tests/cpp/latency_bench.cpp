@@ -22,6 +22,10 @@
 //   steady state: RS(6,3), target 1, parity 6 present, R calls.
 // Every GPU result is compared with the CPU's bytes (outside the timed region).
 //
+// LAT_POOL_ALL=1: every reply is a pool buffer, whatever its size -- blb's rpc pool patched to
+// pool requests of <= 128 KiB + ExtraRoom too (blbrs_buffer_get serves them from its small
+// class), so small replies are read in place instead of staged.
+//
 //   usage: latency_bench SIZE [R] [T]     (one size per process: plans are per process)
 #include <algorithm>
 #include <chrono>
@@ -58,6 +62,10 @@ void check(int rc, const char* what) {
 }
 
 constexpr size_t kSmallMax = (size_t{128} << 10) + (size_t{64} << 10);  // pool.go:31
+const bool kPoolAll = [] {
+    const char* e = std::getenv("LAT_POOL_ALL");
+    return e && *e && *e != '0';
+}();
 
 // One stripe of class (k, m) at piece length L: pieces as blb's RPC layer hands them over.
 struct Stripe {
@@ -65,10 +73,12 @@ struct Stripe {
     size_t L;
     std::vector<uint8_t*> piece;  // k + m
     bool pooled;
-    Stripe(int k_, int m_, size_t L_, std::mt19937_64& rng) : k(k_), m(m_), L(L_), piece(k_ + m_), pooled(L_ > kSmallMax) {
+    size_t cap = 0;               // bytes each piece holds (a pool class can exceed L)
+    Stripe(int k_, int m_, size_t L_, std::mt19937_64& rng)
+        : k(k_), m(m_), L(L_), piece(k_ + m_), pooled(kPoolAll || L_ > kSmallMax) {
+        cap = (L + 63) / 64 * 64;
         for (auto& p : piece) {
             if (pooled) {
-                size_t cap = 0;
                 check(blbrs_buffer_get(L, &p, &cap), "buffer_get");
             } else {
                 p = static_cast<uint8_t*>(std::aligned_alloc(64, (L + 63) / 64 * 64));
@@ -237,7 +247,7 @@ int main(int argc, char** argv) {
     // The steady-state rows above reuse one stripe, so the CPU side runs cache-hot there.
     {
         constexpr size_t kColdBytes = size_t{768} << 20;  // > the 256 MB L3 of the box's EPYC 9575F
-        const size_t per = static_cast<size_t>(6 + 3 + 1) * L;
+        const size_t per = static_cast<size_t>(6 + 3) * s.cap + L;  // pieces as allocated + the output
         const int nring = static_cast<int>(std::clamp<size_t>(kColdBytes / per + 1, 8, 20000));
         std::vector<Stripe*> ring;
         std::vector<uint8_t*> outs;
@@ -270,6 +280,6 @@ int main(int argc, char** argv) {
         for (auto* o : outs) std::free(o);
     }
     std::printf("{\"row\": \"check\", \"piece_bytes\": %zu, \"mismatches\": %d, \"inputs\": \"%s\"}\n", L, bad,
-                L > kSmallMax ? "pool (pinned)" : "pageable");
+                s.pooled ? "pool (pinned)" : "pageable");
     return bad ? 2 : 0;
 }
