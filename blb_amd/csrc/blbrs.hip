@@ -51,6 +51,51 @@ using rt::round_up;
 
 #define HIP_TRY(expr) BLBRS_HIP_TRY(expr)
 
+// Host-side stage timing of one-stripe host calls, for measurement builds only
+// (tools/host_timing.sh: -DBLBRS_HOST_TIMING; the library build compiles HT() to nothing).
+// Marks: 0 blbrs_new entry, 1 its return, 2 the call's checks and plan lookup done, 3 the device
+// and lane picked, 4 worker, device plans and shard classification done, 5 inputs staged and
+// the table tagged, 6 launched, 7 the kernels' completion seen, 8 outputs copied out,
+// 9 blbrs_free returned.  Per-stage medians go to stderr at exit.
+#ifdef BLBRS_HOST_TIMING
+namespace ht {
+constexpr int kMarks = 10;
+thread_local std::chrono::steady_clock::time_point g_t[kMarks];
+thread_local int g_next = 0;
+std::mutex g_mu;
+std::vector<std::vector<double>> g_us(kMarks);
+inline void mark(int i) {
+    if (i == 0) g_next = 0;
+    if (i != g_next) {  // out of order (another path): drop this call
+        g_next = -1;
+        return;
+    }
+    g_t[i] = std::chrono::steady_clock::now();
+    g_next = i + 1;
+    if (i == kMarks - 1) {
+        std::lock_guard<std::mutex> g(g_mu);
+        for (int j = 1; j < kMarks; ++j)
+            g_us[j].push_back(std::chrono::duration<double, std::micro>(g_t[j] - g_t[j - 1]).count());
+    }
+}
+struct Dump {
+    ~Dump() {
+        std::lock_guard<std::mutex> g(g_mu);
+        std::fprintf(stderr, "{\"host_timing_us_p50\": [");
+        for (int j = 1; j < kMarks; ++j) {
+            auto v = g_us[j];
+            std::sort(v.begin(), v.end());
+            std::fprintf(stderr, "%s%.3f", j > 1 ? ", " : "", v.empty() ? -1.0 : v[v.size() / 2]);
+        }
+        std::fprintf(stderr, "], \"calls\": %zu}\n", g_us[1].size());
+    }
+} g_dump;
+}  // namespace ht
+#define HT(i) ht::mark(i)
+#else
+#define HT(i) ((void)0)
+#endif
+
 namespace {
 
 // ---------------------------------------------------------------------------------------
@@ -496,8 +541,10 @@ struct Step {
 // sees what an earlier one wrote (Reconstruct then Verify = reconstructAndVerify,
 // store.go:1132-1142, in one device round trip).  Shards read by a step and not produced by
 // an earlier step are copied in once; shards written by store steps are copied out.
+// `known` (one stripe, optional): the caller's device views of the n shards (0 = pageable), so
+// each shard's pointer attributes are looked up once per call.
 int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const* shards, size_t batch, size_t S,
-             int* ok, int dev) {
+             int* ok, int dev, const uint64_t* known = nullptr) {
     rt::WorkerLease w;
     int rc = w.acquire(dev);
     if (rc) return rc;
@@ -570,7 +617,8 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         for (int i = 0; i < n; ++i) {
             if (!touched[i]) continue;
             int owner = -1;
-            const bool visible = rt::device_view(shards[b * n + i], &view[b * n + i], &owner);
+            const bool visible = known && batch == 1 ? (view[i] = known[i]) != 0
+                                                     : rt::device_view(shards[b * n + i], &view[b * n + i], &owner);
             if (!visible) {
                 pageable[b * n + i] = 1;
                 ++ns;
@@ -580,6 +628,7 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     }
     if (max_staged == 0) {
         // Everything in place: one launch per step over the whole batch.
+        HT(4);
         Stripes st;
         st.nshards = n;
         st.fault = w->fault;
@@ -595,7 +644,9 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         hipError_t e = hipSuccess;
         if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
         if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
+        HT(5);
         const uint32_t seq = launch_steps(st, batch, S, &rc);
+        HT(6);
         if (rc) return drain(rc);
         if (use_done) {
             if ((rc = w->wait_done(seq))) return drain(rc);
@@ -606,8 +657,10 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             if (e == hipSuccess) e = f;
             if (e != hipSuccess) return drain(hip_fail(e, "zero-copy call"));
         }
+        HT(7);
         if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
         if (ok) *ok = verify && *w->flag_host ? 0 : 1;
+        HT(8);
         return BLBRS_OK;
     }
     // Pageable shards are never handed to HIP's copy engines: HIP pins pageable memory on the
@@ -628,6 +681,7 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     const size_t Sb = round_up(S, 256);
     for (size_t x = 0; x < batch * n; ++x) bounce_bytes += pageable[x] ? Sb : 0;
     if (bounce_bytes <= rt::kBounceMaxBytes) {
+        HT(4);
         if ((rc = w->ensure_bounce(bounce_bytes))) return rc;
         uint8_t* const hb = w->bounce;
         std::vector<size_t> at(batch * n, 0);
@@ -658,7 +712,9 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
         hipError_t e = hipSuccess;
         if (verify) e = hipMemsetAsync(w->flag, 0, sizeof(int32_t), w->s[0]);
         if (e != hipSuccess) return drain(hip_fail(e, "hipMemsetAsync"));
+        HT(5);
         const uint32_t seq = launch_steps(st, batch, S, &rc);
+        HT(6);
         if (rc) return drain(rc);
         if (use_done) {
             if ((rc = w->wait_done(seq))) return drain(rc);
@@ -668,6 +724,7 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
             if (e == hipSuccess) e = f;
             if (e != hipSuccess) return drain(hip_fail(e, "staged call"));
         }
+        HT(7);
         if ((rc = rt::check_fault(w->fault, "host call"))) return rc;
         for (size_t b = 0; b < batch; ++b)
             for (int i = 0; i < n; ++i) {
@@ -675,6 +732,7 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
                 if (touched[i] && pageable[x] && is_out[i]) std::memcpy(shards[x], hb + at[x], S);
             }
         if (ok) *ok = verify && *w->flag_host ? 0 : 1;
+        HT(8);
         return BLBRS_OK;
     }
     // Larger calls: units of (stripe, column chunk) alternate over two slots of the staging, in
@@ -792,10 +850,10 @@ int host_call(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const
     // Device-memory shards pin the call to their device; they must all be on one device
     // (a kernel dereferencing another GPU's HBM would need peer access).
     int dev = -1;
+    uint64_t known[256] = {};  // n <= 256 (blbrs_new); 0 = pageable (or NULL)
     for (int i = 0; i < n; ++i) {
-        uint64_t view = 0;
         int owner = -1;
-        if (shards[i] && rt::device_view(shards[i], &view, &owner) && owner >= 0) {
+        if (shards[i] && rt::device_view(shards[i], &known[i], &owner) && owner >= 0) {
             if (dev >= 0 && owner != dev) return fail(BLBRS_ERR_INVALID_ARG, "shards on different devices");
             dev = owner;
         }
@@ -815,7 +873,8 @@ int host_call(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const
     ticket.take(dev, occ, static_cast<uint64_t>(n) * S);
     rt::DeviceGuard guard;
     if ((rc = guard.enter(dev))) return rc;
-    return host_run(enc, steps, shards, 1, S, ok, dev);
+    HT(3);
+    return host_run(enc, steps, shards, 1, S, ok, dev, known);
 }
 
 std::vector<uint8_t> present_vec(const blbrs_encoder* enc, const uint8_t* present) {
@@ -1214,7 +1273,10 @@ static int new_encoder(int data_shards, int parity_shards, std::vector<int> devi
 }
 
 int blbrs_new(int data_shards, int parity_shards, blbrs_encoder** out) {
-    return new_encoder(data_shards, parity_shards, {}, out);
+    HT(0);
+    const int rc = new_encoder(data_shards, parity_shards, {}, out);
+    HT(1);
+    return rc;
 }
 
 int blbrs_new_on(int data_shards, int parity_shards, const int* devices, int ndevices, blbrs_encoder** out) {
@@ -1251,7 +1313,10 @@ int blbrs_set_default_devices(const int* devices, int ndevices) {
     return rt::set_default_devices(std::vector<int>(devices, devices + ndevices));
 }
 
-void blbrs_free(blbrs_encoder* enc) { delete enc; }
+void blbrs_free(blbrs_encoder* enc) {
+    delete enc;
+    HT(9);
+}
 int blbrs_data_shards(const blbrs_encoder* enc) { return enc ? enc->k : 0; }
 int blbrs_parity_shards(const blbrs_encoder* enc) { return enc ? enc->m : 0; }
 
@@ -1417,6 +1482,7 @@ static int reconstruct_host(blbrs_encoder* enc, uint8_t* const* shards, size_t* 
     else if (!hp->out_idx.empty()) steps.push_back(Step{plan_key(false, present, data_only), hp.get(), Mode::kStore});
     else if (verify_ok) steps.push_back(Step{"E", ep.get(), Mode::kVerify});
     if (steps.empty()) return BLBRS_OK;  // data_only with only parity missing
+    HT(2);
     rc = host_call(enc, steps, shards, S, verify_ok);
     if (rc) return rc;
     for (int32_t i : hp->out_idx) lens[i] = S;
