@@ -23,6 +23,10 @@ keeps blb's pool as it is and pins the buffers the pool creates instead:
     buffer.
   * gc(): what a Go GC cycle does to a sync.Pool -- the idle buffers are dropped (and so
     unregistered once nothing else holds them).
+  * set_pool_small(True) (off by default, as in pool.go): requests of up to 128 KiB + ExtraRoom
+    also come from a pool of registered buffers of that size, so small replies are coded in
+    place instead of staged by CPU copies (a 64 KiB degraded read 33 -> 26 us, 128 KiB
+    53 -> 37 us cold).  The Go shim's rsgpu.SetPoolSmall is the same.
 """
 from __future__ import annotations
 
@@ -42,7 +46,8 @@ _PAGE = 4096
 # Reentrant: a finalizer (_unregister) runs whenever the last view of a buffer is dropped,
 # which can happen while this thread holds the lock.
 _mu = threading.RLock()
-_free: dict[int, list] = {c: [] for c in CLASSES}   # sync.Pool contents per class
+_free: dict[int, list] = {c: [] for c in CLASSES + (SMALL_MAX,)}   # sync.Pool contents per class
+_pool_small = False                                 # set_pool_small
 _pinned: set[int] = set()                           # base addresses currently registered
 stats = {"registered": 0, "refused": 0, "unregistered": 0, "reregistered": 0,
          "register_s": 0.0, "unregister_s": 0.0}   # wall time inside blbrs_buffer_(un)register
@@ -100,11 +105,18 @@ def _class_base(b: np.ndarray):
     return owner[off:off + size]
 
 
+def set_pool_small(on: bool) -> None:
+    """Pool (and pin) requests of up to 128 KiB + ExtraRoom too; off restores pool.go's plain
+    buffers for them (buffers already handed out keep their class)."""
+    global _pool_small
+    _pool_small = bool(on)
+
+
 def GetBuffer(n: int) -> np.ndarray:
     """A []byte with length n; NOT zeroed (pool.go:28-43)."""
-    if n <= SMALL_MAX or n > CLASSES[-1]:
+    if n <= 0 or (n <= SMALL_MAX and not _pool_small) or n > CLASSES[-1]:
         return np.empty(max(n, 0), np.uint8)
-    size = next(c for c in CLASSES if n <= c)
+    size = SMALL_MAX if n <= SMALL_MAX else next(c for c in CLASSES if n <= c)
     with _mu:
         base = _free[size].pop() if _free[size] else None
         again = base is not None and base.ctypes.data not in _pinned

@@ -129,7 +129,7 @@ func SetWorkerLimit(perDevice int) error {
 // (SetPinnedLimit): past it registration is refused and the buffer stays pageable -- correct,
 // only staged by the engine -- and is registered again when the pool hands it out later.
 // Small (<= 128 KiB + ExtraRoom) and large (> the 8 MiB class) requests get make(), as in
-// pool.go.  The engine keeps the registered address only while the buffer is alive, and only
+// pool.go -- small ones come from a pinned class pool too after SetPoolSmall(true).  The engine keeps the registered address only while the buffer is alive, and only
 // coding calls (during which the caller holds the slice) touch the memory.
 
 const (
@@ -141,7 +141,11 @@ const (
 )
 
 var (
-	buf8MBPool = sync.Pool{New: func() interface{} { return newPinned(buf8MBSize) }}
+	// SetPoolSmall: requests of up to smallMax come from a pool too (off by default, as in
+	// pool.go).
+	poolSmall    atomic.Bool
+	bufSmallPool = sync.Pool{New: func() interface{} { return newPinned(smallMax) }}
+	buf8MBPool   = sync.Pool{New: func() interface{} { return newPinned(buf8MBSize) }}
 	buf4MBPool = sync.Pool{New: func() interface{} { return newPinned(buf4MBSize) }}
 	buf1MBPool = sync.Pool{New: func() interface{} { return newPinned(buf1MBSize) }}
 	// The class buffers this pool allocated, by base address (a uintptr key keeps nothing
@@ -192,6 +196,9 @@ func getClass(pool *sync.Pool, n int) []byte {
 // limit allows.
 func GetBuffer(n int) []byte {
 	if n <= smallMax {
+		if n > 0 && poolSmall.Load() {
+			return getClass(&bufSmallPool, n)
+		}
 		return make([]byte, n)
 	} else if n <= buf1MBSize {
 		return getClass(&buf1MBPool, n)
@@ -210,6 +217,10 @@ func PutBuffer(b []byte, exclusive bool) {
 		return
 	}
 	switch cap(b) {
+	case smallMax:
+		if poolSmall.Load() {
+			bufSmallPool.Put(&b)
+		}
 	case buf8MBSize:
 		buf8MBPool.Put(&b)
 	case buf4MBSize:
@@ -218,6 +229,12 @@ func PutBuffer(b []byte, exclusive bool) {
 		buf1MBPool.Put(&b)
 	}
 }
+
+// SetPoolSmall makes GetBuffer pool (and pin) requests of up to 128 KiB + ExtraRoom as well,
+// which pool.go hands out as plain make() buffers.  Small replies are then coded in place
+// instead of staged by CPU copies: a 64 KiB degraded read 33 -> 26 us, 128 KiB 53 -> 37 us
+// with cold inputs (DESIGN.md §4d round 6; blb_amd/rpc.py set_pool_small is the same rule).
+func SetPoolSmall(on bool) { poolSmall.Store(on) }
 
 // SetPinnedLimit caps the bytes pinned at once (blbrs_pool_set_live_limit; default 16 GiB,
 // 0 = no cap).  Buffers the pool creates beyond it are plain Go memory.

@@ -51,6 +51,25 @@ def test_rpc_pool_classes_like_pool_go():
     rpc.gc()
 
 
+def test_rpc_pool_small_class_opt_in():
+    """set_pool_small(True): requests of up to 128 KiB + ExtraRoom come from a pool of their own
+    class (reused after an exclusive Put); with it off (pool.go's rule, the default) they are
+    plain buffers again."""
+    try:
+        rpc.set_pool_small(True)
+        a = rpc.GetBuffer(4096)
+        base = rpc._class_base(a)
+        assert base is not None and base.size == rpc.SMALL_MAX and a.size == 4096
+        rpc.PutBuffer(a, True)
+        b = rpc.GetBuffer(rpc.SMALL_MAX)
+        assert b.ctypes.data == a.ctypes.data and b.size == rpc.SMALL_MAX   # reused
+        assert rpc.GetBuffer(0).size == 0
+    finally:
+        rpc.set_pool_small(False)
+        rpc.gc()
+    assert rpc._class_base(rpc.GetBuffer(4096)) is None
+
+
 def test_pool_live_limit_refuses_before_pinning():
     """blbrs_buffer_get past the live limit is ErrLimit (checked before any allocation, so this
     runs without a GPU); registration with no device releases its reservation."""
@@ -254,6 +273,37 @@ class _PoolReader:
     def collect(self):
         with self.lock:
             self.held.clear()
+
+
+@pytest.mark.gpu
+def test_pool_small_replies_coded_in_place():
+    """With small replies pooled (rpc.set_pool_small), a 64 KiB degraded read's replies are
+    registered buffers -- coded in place, not staged -- and the rebuilt piece is bit-exact
+    against the restatement."""
+    from oracle import rs_numpy as N
+    k, m, S = 6, 3, 64 << 10
+    rng = np.random.default_rng(64)
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+    full = data + list(N.encode(k, m, data))
+    try:
+        rpc.set_pool_small(True)
+        sh = []
+        for i in range(k + m):
+            b = rpc.GetBuffer(S)
+            b[:] = full[i]
+            sh.append(b)
+        assert all(rpc.is_pinned(b) for b in sh)
+        enc = rs.New(k, m)
+        for lost in (1, 4):
+            work = list(sh)
+            work[lost] = None
+            enc.ReconstructData(work)
+            assert np.array_equal(work[lost], full[lost]), lost
+        for b in sh:
+            rpc.PutBuffer(b, True)
+    finally:
+        rpc.set_pool_small(False)
+        rpc.gc()
 
 
 @pytest.mark.gpu
