@@ -51,9 +51,18 @@ int main(int argc, char** argv) {
                     T * static_cast<double>(N) / el);
         (void)hipHostFree(p);
     }
-    const std::vector<size_t> lengths =
+    std::vector<size_t> lengths =
         encode ? std::vector<size_t>{size_t{64} << 10, size_t{256} << 10, size_t{1} << 20, size_t{4} << 20}
                : std::vector<size_t>{size_t{4} << 10, size_t{16} << 10, size_t{64} << 10, size_t{256} << 10, size_t{1} << 20};
+    if (const char* e = std::getenv("BB_LENGTHS")) {  // e.g. "131072,262144"
+        lengths.clear();
+        for (const char* p = e; *p;) {
+            char* end = nullptr;
+            lengths.push_back(std::strtoull(p, &end, 0));
+            p = *end == ',' ? end + 1 : end;
+            if (end == p && *p) break;
+        }
+    }
     for (size_t L : lengths) {
         // Per-thread pinned stripe + output.
         std::vector<uint8_t*> bufs(static_cast<size_t>(T) * (n + 1));
