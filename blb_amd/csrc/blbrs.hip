@@ -584,7 +584,8 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     // to copy back; otherwise on a stream wait.
     size_t call_bytes = 0;
     for (int i = 0; i < n; ++i) call_bytes += touched[i] ? batch * S : 0;
-    const bool use_done = !verify && call_bytes <= rt::kDoneMaxBytes && tune::get(tune::kDoneWord) != 0;
+    const bool use_done =
+        !verify && S <= rt::kDoneMaxPiece && call_bytes <= rt::kDoneMaxBytes && tune::get(tune::kDoneWord) != 0;
     auto launch_steps = [&](const Stripes& st, size_t nb, size_t len, int* rc_out) {
         uint32_t seq = 0;
         if (use_done) {

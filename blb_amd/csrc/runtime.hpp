@@ -150,7 +150,12 @@ constexpr size_t kPinnedSlotBytes = size_t{8} << 20;
 // default on): the word arrives ~3 us before the stream's completion signal would wake the
 // caller (tools/sync_probe.hip).  The spin bound covers such a kernel many times
 // over; past it the thread waits for the stream.
+// Pieces above kDoneMaxPiece keep rs_code_kernel and the stream wait: from 128 KiB a single
+// caller gains nothing (128 KiB ties, 256 KiB is 2-5 us slower) and 64 concurrent per-call
+// callers lose 20-31 % of their calls/s, while up to 64 KiB the word saves 4.5-7 us a call and
+// costs concurrent callers at most 5-10 % at 64 KiB (profiles/r06/concurrency/).
 constexpr size_t kDoneMaxBytes = size_t{2} << 20;
+constexpr size_t kDoneMaxPiece = size_t{64} << 10;
 constexpr int kDoneSpinUs = 2000;
 
 struct Worker {

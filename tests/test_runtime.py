@@ -333,8 +333,9 @@ def test_gpu_per_read_new_builds_each_plan_once():
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m", [(6, 3), (10, 3), (12, 5)])
 def test_gpu_small_calls_end_on_completion_word(knob, k, m):
-    """Small single-launch host calls with no verify flag run on rs_small_kernel and end on its
-    completion word (rs_small.hpp, runtime.hpp kDoneMaxBytes): Encode, ReconstructData and
+    """Small single-launch host calls (pieces of at most 64 KiB) with no verify flag run on the
+    small-call kernels and end on their completion word (rs_small.hpp, runtime.hpp
+    kDoneMaxPiece / kDoneMaxBytes): Encode, ReconstructData and
     Reconstruct of pageable (staged) and pool (in place) shards, whole 4 KiB chunks and ragged
     ends, are bit-exact against the restatement; each call counts one done wait and none falls
     back to the stream wait.  Verify, and BLBRS_DONE_WORD = 0, wait for the stream and count
@@ -345,7 +346,7 @@ def test_gpu_small_calls_end_on_completion_word(knob, k, m):
     rng = np.random.default_rng(k * 100 + m)
     before = rs.device_stats(0)
     calls = 0
-    for S in (4096, 12000, 65536, 98765):
+    for S in (4096, 12000, 40000, 65536):
         data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
         full = data + list(N.encode(k, m, data))
         for pooled in (False, True):
@@ -394,6 +395,14 @@ def test_gpu_small_calls_end_on_completion_word(knob, k, m):
     assert mid["done_fallbacks"] == before["done_fallbacks"]
     assert mid["done_waits"] - before["done_waits"] == calls, (before, mid, calls)
     enc = rs.New(k, m)
+    # Pieces above 64 KiB (runtime.hpp kDoneMaxPiece) keep rs_code_kernel and the stream wait.
+    S = 98765
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+    full = data + list(N.encode(k, m, data))
+    sh = [f.copy() for f in full]
+    sh[0] = None
+    enc.ReconstructData(sh)
+    assert np.array_equal(sh[0], full[0])
     S = 4096
     data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
     full = data + list(N.encode(k, m, data))
