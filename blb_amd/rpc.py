@@ -25,8 +25,8 @@ keeps blb's pool as it is and pins the buffers the pool creates instead:
     unregistered once nothing else holds them).
   * set_pool_small(True) (off by default, as in pool.go): requests of up to 128 KiB + ExtraRoom
     also come from a pool of registered buffers of that size, so small replies are coded in
-    place instead of staged by CPU copies (a 64 KiB degraded read 33 -> 26 us, 128 KiB
-    53 -> 37 us cold).  The Go shim's rsgpu.SetPoolSmall is the same.
+    place instead of staged by CPU copies (a 64 KiB degraded read 31 -> 25 us, 128 KiB
+    53 -> 41 us cold).  The Go shim's rsgpu.SetPoolSmall is the same.
 """
 from __future__ import annotations
 

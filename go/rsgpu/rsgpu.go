@@ -232,7 +232,7 @@ func PutBuffer(b []byte, exclusive bool) {
 
 // SetPoolSmall makes GetBuffer pool (and pin) requests of up to 128 KiB + ExtraRoom as well,
 // which pool.go hands out as plain make() buffers.  Small replies are then coded in place
-// instead of staged by CPU copies: a 64 KiB degraded read 33 -> 26 us, 128 KiB 53 -> 37 us
+// instead of staged by CPU copies: a 64 KiB degraded read 31 -> 25 us, 128 KiB 53 -> 41 us
 // with cold inputs (DESIGN.md §4d round 6; blb_amd/rpc.py set_pool_small is the same rule).
 func SetPoolSmall(on bool) { poolSmall.Store(on) }
 
