@@ -584,14 +584,12 @@ int host_run(blbrs_encoder* enc, const std::vector<Step>& steps, uint8_t* const*
     // to copy back; otherwise on a stream wait.
     size_t call_bytes = 0;
     for (int i = 0; i < n; ++i) call_bytes += touched[i] ? batch * S : 0;
-    const bool use_done =
+    bool use_done =
         !verify && S <= rt::kDoneMaxPiece && call_bytes <= rt::kDoneMaxBytes && tune::get(tune::kDoneWord) != 0;
+    if (use_done && w->ensure_done() != BLBRS_OK) use_done = false;  // no word to spin on: the stream wait
     auto launch_steps = [&](const Stripes& st, size_t nb, size_t len, int* rc_out) {
-        uint32_t seq = 0;
-        if (use_done) {
-            if ((*rc_out = w->ensure_done())) return seq;
-            seq = w->next_done_seq();
-        }
+        *rc_out = BLBRS_OK;
+        const uint32_t seq = use_done ? w->next_done_seq() : 0;
         for (size_t t = 0; t < steps.size(); ++t) {
             Stripes x = st;
             x.small = use_done;
